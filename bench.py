@@ -1,0 +1,261 @@
+"""bench.py -- device-resident TLS record seal/open throughput on MI355X.
+
+Metric (BASELINE.json): GiB/s device-resident record seal/open, AES-128-GCM +
+ChaCha20-Poly1305, 16 KiB records.  Workload: BASELINE configs[1] and [2]
+(single session key, 2^20 x 16 KiB TLS 1.3 records per GPU, nonce = iv xor
+seq, 5-byte AAD) -- one "step" seals the whole batch and opens it back, for
+AES-128-GCM and for ChaCha20-Poly1305 (4 kernel launches, 4 x 16 GiB of
+payload).  ``value`` = payload bytes (plaintext for seal, same L for open)
+of all ranks / max-over-ranks time, in GiB/s.
+
+Multi-GPU (``torch.distributed.run``): every rank seals its own contiguous
+seq range (weak scaling); the only collective is an RCCL all-reduce of the
+per-rank counters {records, payload bytes, auth failures} and the timing max.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--records R] [--len L]
+"""
+import argparse
+import json
+import multiprocessing as mp
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+for _p in (ROOT, os.path.join(ROOT, "tlslite-ng_amd"), os.path.join(ROOT, "tests", "golden")):
+    if _p not in sys.path:
+        sys.path.insert(0, _p)
+
+HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec, /opt/skills/guides/MI355X_MICROARCH.md
+AAD_LEN = 5
+NONCE_LEN = 12
+TAG_LEN = 16
+
+
+def algorithmic_bytes(n, L, op):
+    """seal reads L + A + 12, writes L + 16; open reads
+    L + 16 + A + 12, writes L (+1 status byte)."""
+    per = 2 * L + AAD_LEN + NONCE_LEN + TAG_LEN + (1 if op == "open" else 0)
+    return n * per
+
+
+# ------------------------------------------------------------- CPU baseline
+
+def _cpu_worker(args):
+    nrec, L, seed = args
+    sys.path.insert(0, ROOT)
+    import numpy as np
+    from oracle import pyaead
+    from vectors import tls13_aad, tls13_nonce
+    rng = np.random.default_rng(seed)
+    t0 = time.perf_counter()
+    done = 0
+    for alg in ("aes128gcm", "chacha20-poly1305"):
+        key = rng.bytes(16 if alg == "aes128gcm" else 32)
+        iv = rng.bytes(12)
+        c = pyaead.AESGCM(key) if alg == "aes128gcm" else pyaead.CHACHA20_POLY1305(key)
+        for i in range(nrec):
+            pt = rng.bytes(L)
+            nonce = tls13_nonce(iv, i)
+            aad = tls13_aad(L)
+            sealed = c.seal(nonce, pt, aad)
+            assert c.open(nonce, sealed, aad) == pt
+            done += 2 * L
+    return done, time.perf_counter() - t0
+
+
+def cpu_baseline(L, cores, nrec):
+    """The reference's pure-Python path (oracle/pyaead.py restates it; it runs
+    at 0.6-1.0x the reference's own per-core speed) on ``cores``
+    host processes, seal+open of ``nrec`` records per algorithm per process."""
+    ctx = mp.get_context("spawn")
+    t0 = time.perf_counter()
+    with ctx.Pool(cores) as pool:
+        res = pool.map(_cpu_worker, [(nrec, L, 1000 + c) for c in range(cores)])
+    wall = time.perf_counter() - t0
+    total = sum(r[0] for r in res)
+    return {"value": total / wall / 2 ** 30, "unit": "GiB/s", "cores": cores, "kind": "port",
+            "sample": "%d procs x %d x %d B records, AES-128-GCM + ChaCha20-Poly1305 seal+open, "
+                      "oracle/pyaead.py (pure-Python restatement of the reference path); "
+                      "%.1f s wall" % (cores, nrec, L, wall)}
+
+
+# -------------------------------------------------------------- GPU bench
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--records", type=int, default=1 << 20)
+    ap.add_argument("--len", type=int, default=16384)
+    ap.add_argument("--cpu-cores", type=int, default=16)
+    ap.add_argument("--cpu-records", type=int, default=6)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--e2e", action="store_true", help="also time the host<->device path")
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+    import tlsgpu
+    from vectors import tls13_aad
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    n, L = args.records, args.len
+    dev = "cuda"
+    g = torch.Generator(device=dev).manual_seed(0x7715 + rank)
+    inp = torch.randint(0, 256, (n * L,), dtype=torch.uint8, device=dev, generator=g)
+    sealed = torch.empty(n * (L + TAG_LEN), dtype=torch.uint8, device=dev)
+    back = torch.empty(n * L, dtype=torch.uint8, device=dev)
+    status = torch.zeros(n, dtype=torch.uint8, device=dev)
+    nonces = torch.empty(NONCE_LEN * n, dtype=torch.uint8, device=dev)
+    aad = torch.tensor(list(tls13_aad(L)), dtype=torch.uint8, device=dev)
+    hrng = torch.Generator().manual_seed(0x7716)
+    iv = bytes(torch.randint(0, 256, (12,), dtype=torch.uint8, generator=hrng).tolist())
+    keys = {"aes128gcm": bytes(torch.randint(0, 256, (16,), dtype=torch.uint8, generator=hrng).tolist()),
+            "chacha20-poly1305": bytes(torch.randint(0, 256, (32,), dtype=torch.uint8,
+                                                     generator=hrng).tolist())}
+    ciphers = {"aes128gcm": tlsgpu.HipAESGCM(bytearray(keys["aes128gcm"])),
+               "chacha20-poly1305": tlsgpu.HipCHACHA20_POLY1305(bytearray(keys["chacha20-poly1305"]))}
+    # this rank's records are seq [rank*n, (rank+1)*n) of one connection
+    tlsgpu.make_nonces(iv, rank * n, n, nonces)
+    seal_b = tlsgpu.make_batch(n, inp, sealed, nonces, aad=aad, fixed_len=L, in_stride=L,
+                               out_stride=L + TAG_LEN, fixed_aad_len=AAD_LEN)
+    open_b = tlsgpu.make_batch(n, sealed, back, nonces, aad=aad, fixed_len=L,
+                               in_stride=L + TAG_LEN, out_stride=L, fixed_aad_len=AAD_LEN,
+                               status=status)
+    stream = torch.cuda.current_stream()
+    kinds = [(a, op) for a in ciphers for op in ("seal", "open")]
+    ev = {k: [] for k in kinds}
+
+    def step(record):
+        for a, c in ciphers.items():
+            for op, fn, b in (("seal", tlsgpu.seal_batch, seal_b), ("open", tlsgpu.open_batch, open_b)):
+                if record:
+                    e0 = torch.cuda.Event(enable_timing=True)
+                    e1 = torch.cuda.Event(enable_timing=True)
+                    e0.record(stream)
+                fn(c, b, stream)
+                if record:
+                    e1.record(stream)
+                    ev[(a, op)].append((e0, e1))
+
+    for _ in range(args.warmup):
+        step(False)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step(True)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+
+    # correctness of the timed work (not timed): every record authentic, round trip exact
+    ok = int(status.sum().item()) == n and torch.equal(back, inp)
+    counters = torch.tensor([float(n * args.steps * len(kinds)),
+                             float(n * L * args.steps * len(kinds)),
+                             float(n - int(status.sum().item())), elapsed], dtype=torch.float64,
+                            device=dev)
+    if world > 1:
+        tmax = counters[3:4].clone()
+        dist.all_reduce(counters, op=dist.ReduceOp.SUM)
+        dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
+        elapsed = float(tmax.item())
+    payload_bytes = float(counters[1].item())
+    per_kernel = {}
+    for (a, op), lst in ev.items():
+        ms = sum(e0.elapsed_time(e1) for e0, e1 in lst) / len(lst)
+        alg_bytes = algorithmic_bytes(n, L, op)
+        per_kernel["%s_%s" % (a, op)] = {
+            "ms": round(ms, 3), "payload_GiBps": round(n * L / (ms / 1e3) / 2 ** 30, 1),
+            "algorithmic_GBps": round(alg_bytes / (ms / 1e3) / 1e9, 1)}
+    dom = max(per_kernel, key=lambda k: per_kernel[k]["ms"])
+    dom_op = "open" if dom.endswith("open") else "seal"
+    dom_achieved = algorithmic_bytes(n, L, dom_op) / (per_kernel[dom]["ms"] / 1e3) / 1e9
+
+    e2e = None
+    if args.e2e and rank == 0:
+        e2e = end_to_end(torch, tlsgpu, ciphers, aad, nonces, L, min(n, 1 << 16))
+
+    if rank == 0:
+        line = {
+            "metric": "GiB/s device-resident record seal/open, AES-128-GCM + ChaCha20-Poly1305 16KiB",
+            "value": round(payload_bytes / elapsed / 2 ** 30, 2),
+            "unit": "GiB/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u8",
+            "data": "synthetic (torch.randint payloads, seeded per rank)",
+            "config": {"workload": "BASELINE configs[1]+[2]: 2^20 x 16 KiB TLS 1.3 records per GPU, "
+                                   "single key, AES-128-GCM and ChaCha20-Poly1305, seal+open",
+                       "records_per_gpu": n, "record_len": L, "aad_len": AAD_LEN,
+                       "parallelism": "records sharded by seq range, %d rank(s)" % world},
+            "per_kernel": per_kernel,
+            "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(dom_achieved, 1),
+                         "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(dom_achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                         "bytes_per_record": algorithmic_bytes(1, L, dom_op)},
+            "verified": bool(ok),
+            "auth_failures": int(counters[2].item()),
+        }
+        if e2e:
+            line["end_to_end"] = e2e
+        if not args.no_cpu_baseline and world == 1:
+            line["cpu_baseline"] = cpu_baseline(L, args.cpu_cores, args.cpu_records)
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+    if not ok:
+        sys.exit(3)
+
+
+def end_to_end(torch, tlsgpu, ciphers, aad, nonces, L, n):
+    """Records start and end in pinned host memory (socket buffers): H2D copy,
+    seal, D2H copy, pipelined over chunks on two streams.  Reported in
+    DESIGN.md, never as ``value``."""
+    chunk = 8192
+    host_in = torch.randint(0, 256, (n * L,), dtype=torch.uint8).pin_memory()
+    host_out = torch.empty(n * (L + TAG_LEN), dtype=torch.uint8).pin_memory()
+    res = {}
+    for a, c in ciphers.items():
+        streams = [torch.cuda.Stream() for _ in range(2)]
+        bufs = [(torch.empty(chunk * L, dtype=torch.uint8, device="cuda"),
+                 torch.empty(chunk * (L + TAG_LEN), dtype=torch.uint8, device="cuda"))
+                for _ in streams]
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for ci, s0 in enumerate(range(0, n, chunk)):
+            k = min(chunk, n - s0)
+            s = streams[ci % 2]
+            din, dout = bufs[ci % 2]
+            with torch.cuda.stream(s):
+                din[:k * L].copy_(host_in[s0 * L:(s0 + k) * L], non_blocking=True)
+                b = tlsgpu.make_batch(k, din, dout, nonces[12 * s0:], aad=aad, fixed_len=L,
+                                      in_stride=L, out_stride=L + TAG_LEN, fixed_aad_len=AAD_LEN)
+                tlsgpu.seal_batch(c, b, s)
+                host_out[s0 * (L + TAG_LEN):(s0 + k) * (L + TAG_LEN)].copy_(
+                    dout[:k * (L + TAG_LEN)], non_blocking=True)
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t0
+        res[a + "_seal"] = {"GiBps_payload": round(n * L / dt / 2 ** 30, 2), "records": n}
+    return res
+
+
+if __name__ == "__main__":
+    main()

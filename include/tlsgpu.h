@@ -1,0 +1,136 @@
+/*
+ * tlsgpu.h -- C ABI of the MI355X TLS record-layer AEAD engine (libtlsgpu.so).
+ *
+ * This is the drop-in boundary for tlslite-ng's bulk-cipher path.  The
+ * reference binds AEAD objects through tlslite/utils/cipherfactory.py
+ * (createAESGCM :81-100, createCHACHA20 :144-159) and calls
+ * obj.seal(nonce, plaintext, data) / obj.open(nonce, ciphertext, data)
+ * (tlslite/utils/aesgcm.py:101,126; tlslite/utils/chacha20_poly1305.py:48,68)
+ * once per record from tlslite/recordlayer.py:558 (_encryptThenSeal) and
+ * :821 (_decryptAndUnseal).  The ctypes objects in tlsgpu/ (see
+ * INTEGRATION.md) bind exactly the functions below.
+ *
+ * Conventions: plain pointers and sizes, no exceptions across the ABI, every
+ * function returns an int status (TG_OK = 0, negative = error; tg_open
+ * returns 1 = authentic / 0 = rejected).  A key handle is bound to the device
+ * current when it was created and is not thread-safe (one handle per
+ * connection direction, as ConnectionState.encContext is in the reference,
+ * recordlayer.py:239-249).  Batch entry points take DEVICE pointers and are
+ * ordered on the given HIP stream (NULL = the handle's own stream).
+ */
+#ifndef TLSGPU_H
+#define TLSGPU_H
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+#if defined(__GNUC__)
+#pragma GCC visibility push(default)
+#endif
+
+#define TG_OK 0
+#define TG_EINVAL (-22)      /* bad argument (NULL pointer, bad size) */
+#define TG_EKEYLEN (-2)      /* key length: AssertionError (aesgcm.py:37-38) /
+                                ValueError (chacha20_poly1305.py:21-22) */
+#define TG_ENONCE (-3)       /* nonce length != 12: ValueError
+                                (aesgcm.py:107-108, chacha20_poly1305.py:53-54) */
+#define TG_ENOMEM (-12)
+#define TG_EHIP (-5)         /* a HIP runtime call failed; see tg_last_error() */
+#define TG_ENODEV (-19)      /* no GPU visible */
+
+/* Algorithms (the reference's cipher .name values). */
+#define TG_AES_GCM 0          /* "aes128gcm" (16-byte key) / "aes256gcm" (32) */
+#define TG_CHACHA20_POLY1305 1 /* "chacha20-poly1305" (32-byte key) */
+
+typedef struct tg_key tg_key;
+
+/* Library / device. */
+const char* tg_version(void);
+const char* tg_last_error(void);           /* thread-local message of the last error */
+int tg_device_count(int* count);
+int tg_init(int device);                   /* hipSetDevice for the calling thread */
+
+/* Keys -- replaces python_aesgcm.new (python_aesgcm.py:10-11) and
+ * python_chacha20_poly1305.new (python_chacha20_poly1305.py:9-11): expands the
+ * AES round keys and the GHASH tables for H = E_K(0) (aesgcm.py:27-57) on the
+ * host and uploads them once.  nkeys > 1 builds a key table indexed by
+ * tg_batch.key_idx (many sessions in one batch). */
+int tg_key_create(int alg, const uint8_t* keys, size_t keylen, size_t nkeys,
+                  tg_key** out);
+int tg_key_destroy(tg_key* k);
+int tg_key_info(const tg_key* k, int* alg, size_t* keylen, size_t* nkeys);
+
+/* Per-record drop-in, HOST buffers (synchronous).
+ * tg_seal: out receives ct || tag (len + 16 bytes) -- AESGCM.seal /
+ *   CHACHA20_POLY1305.seal.
+ * tg_open: in = ct || tag (inlen bytes); pt receives inlen - 16 bytes.
+ *   Returns 1 when the tag verifies, 0 when the record is rejected (the
+ *   reference's None: bad tag, or inlen < 16), negative on error.
+ *   On rejection pt is zeroed, never left holding unauthenticated bytes. */
+int tg_seal(tg_key* k, const uint8_t* nonce, size_t noncelen,
+            const uint8_t* aad, size_t aadlen, const uint8_t* pt, size_t len,
+            uint8_t* out);
+int tg_open(tg_key* k, const uint8_t* nonce, size_t noncelen,
+            const uint8_t* aad, size_t aadlen, const uint8_t* in, size_t inlen,
+            uint8_t* pt);
+
+/* Batch of records, DEVICE pointers.  Record i:
+ *   payload  in  + (in_off  ? in_off[i]  : i * in_stride),  len[i] bytes
+ *            (seal: plaintext; open: ciphertext, followed by its 16-byte tag)
+ *   output   out + (out_off ? out_off[i] : i * out_stride)
+ *            (seal: ct || tag, len[i] + 16 bytes; open: pt, len[i] bytes)
+ *   nonce    nonce + 12 * i (12 bytes)
+ *   aad      aad + (aad_off ? aad_off[i] : i * aad_stride),
+ *            aad_len ? aad_len[i] : fixed_aad_len bytes
+ *   key      key table entry key_idx ? key_idx[i] : 0
+ *   status   open only: status[i] = 1 authentic / 0 rejected (pt zeroed)
+ * len == NULL means every record is fixed_len bytes.  Offsets with 16-byte
+ * alignment take the vector path; any alignment is accepted.
+ * Records are independent; nothing is ordered between them. */
+typedef struct tg_batch {
+    uint64_t n;
+    const uint8_t* in;
+    const uint64_t* in_off;
+    uint64_t in_stride;
+    const uint32_t* len;
+    uint32_t fixed_len;
+    uint32_t fixed_aad_len;
+    uint8_t* out;
+    const uint64_t* out_off;
+    uint64_t out_stride;
+    const uint8_t* nonce;
+    const uint8_t* aad;
+    const uint64_t* aad_off;
+    uint64_t aad_stride;
+    const uint32_t* aad_len;
+    const uint32_t* key_idx;
+    uint8_t* status;
+} tg_batch;
+
+int tg_seal_batch(tg_key* k, const tg_batch* b, void* stream);
+int tg_open_batch(tg_key* k, const tg_batch* b, void* stream);
+
+/* Build per-record 12-byte nonces on the device from a connection's fixed IV
+ * and sequence numbers, as RecordLayer._getNonce does (recordlayer.py:522-534):
+ *   mode 0 (TLS 1.3 / RFC ChaCha): nonce_i = iv12 xor (0^4 || be64(seq0 + i))
+ *   mode 1 (TLS 1.2 GCM, draft ChaCha): nonce_i = iv4 || be64(seq0 + i)
+ * out: device, 12 * n bytes. */
+int tg_make_nonces(int mode, const uint8_t* iv, size_t ivlen, uint64_t seq0,
+                   uint64_t n, uint8_t* out, void* stream);
+
+/* Device memory helpers so a ctypes host needs no other GPU runtime. */
+int tg_malloc(void** p, size_t bytes);
+int tg_free(void* p);
+int tg_memcpy_h2d(void* dst, const void* src, size_t bytes, void* stream);
+int tg_memcpy_d2h(void* dst, const void* src, size_t bytes, void* stream);
+int tg_stream_sync(void* stream);
+
+#if defined(__GNUC__)
+#pragma GCC visibility pop
+#endif
+#ifdef __cplusplus
+}
+#endif
+#endif

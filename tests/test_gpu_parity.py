@@ -1,0 +1,248 @@
+"""GPU parity: libtlsgpu (HIP, gfx950) against the reference's fixtures and
+the C oracle, bit-exact.  Every call goes through the C ABI.
+"""
+import hashlib
+
+import numpy as np
+import pytest
+
+from vectors import detbytes, load, tls13_aad, tls13_nonce
+
+pytestmark = pytest.mark.gpu
+
+KAT = load("kat.json")
+VECS = load("aead_vectors.json")
+NEG = load("negative.json")
+BATCH = load("record_batch.json")
+H = bytes.fromhex
+
+
+@pytest.fixture(scope="module")
+def torch():
+    import torch as t
+    if not t.cuda.is_available():
+        pytest.fail("GPU tests need a visible MI355X")
+    return t
+
+
+@pytest.fixture(scope="module")
+def tg(torch):
+    import tlsgpu
+    assert tlsgpu.device_count() > 0
+    return tlsgpu
+
+
+def _obj(tg, alg, key):
+    key = bytearray(key)
+    if alg.startswith("chacha"):
+        return tg.createCHACHA20(key, ["hip"])
+    return tg.createAESGCM(key, ["hip"])
+
+
+def _inputs(v):
+    tag = "%s-%d-%d" % (v["alg"], v["len"], v["aadlen"])
+    return (detbytes("key-" + tag, v["keylen"]), detbytes("nonce-" + tag, 12),
+            detbytes("aad-" + tag, v["aadlen"]), detbytes("pt-" + tag, v["len"]))
+
+
+# ------------------------------------------------ per-record drop-in objects
+
+def test_object_contract(tg):
+    a = _obj(tg, "aes128gcm", bytes(16))
+    assert (a.name, a.isAEAD, a.isBlockCipher, a.nonceLength, a.tagLength) == \
+        ("aes128gcm", True, False, 12, 16)
+    assert _obj(tg, "aes256gcm", bytes(32)).name == "aes256gcm"
+    c = _obj(tg, "chacha20-poly1305", bytes(32))
+    assert (c.name, c.implementation) == ("chacha20-poly1305", "hip")
+    import copy
+    c2 = copy.copy(c)
+    del c
+    assert c2.open(bytes(12), c2.seal(bytes(12), b"abc", b""), b"") == b"abc"
+    with pytest.raises(ValueError):
+        a.seal(bytearray(11), bytearray(16), bytearray(0))
+    with pytest.raises(ValueError):
+        c2.open(bytearray(16), bytearray(64), bytearray(0))
+    assert a.open(bytearray(12), bytearray(15), bytearray(0)) is None
+
+
+@pytest.mark.parametrize("i", range(len(KAT["aead"])))
+def test_kat(tg, i):
+    v = KAT["aead"][i]
+    o = _obj(tg, v["alg"], H(v["key"]))
+    got = o.seal(bytearray(H(v["nonce"])), bytearray(H(v["pt"])), bytearray(H(v["aad"])))
+    assert got.hex() == v["ct_tag"]
+    assert o.open(bytearray(H(v["nonce"])), got, bytearray(H(v["aad"]))) == bytearray(H(v["pt"]))
+
+
+def test_golden_grid(tg):
+    for v in VECS:
+        key, nonce, aad, pt = _inputs(v)
+        o = _obj(tg, v["alg"], key)
+        sealed = o.seal(nonce, pt, aad)
+        assert sealed[-16:].hex() == v["tag"], (v["alg"], v["len"], v["aadlen"])
+        assert hashlib.sha256(bytes(sealed[:-16])).hexdigest() == v["ct_sha256"]
+        assert o.open(nonce, sealed, aad) == pt
+
+
+def test_negative(tg):
+    for v in NEG:
+        o = _obj(tg, v["alg"], H(v["key"]))
+        assert o.open(bytearray(H(v["nonce"])), bytearray(H(v["ct_tag"])),
+                      bytearray(H(v["aad"]))) is None, (v["alg"], v["case"])
+
+
+# ----------------------------------------------------------- device batches
+
+def _run_seal_open(torch, tg, oracle_mod, hb, alg, keys, key_obj, tamper=()):
+    d = hb.to_device(torch)
+    tg.seal_batch(key_obj, hb.batch_kwargs(d))
+    torch.cuda.synchronize()
+    got = d["out"].cpu().numpy()
+    want, _ = hb.oracle(oracle_mod, alg, keys, "seal")
+    for i in range(hb.n):
+        o, L = int(hb.out_off[i]), int(hb.lens[i])
+        assert np.array_equal(got[o:o + L + 16], want[o:o + L + 16]), ("seal mismatch", i, L)
+    # open the sealed records back (input = ct||tag at out_off)
+    sealed = got.copy()
+    for i in tamper:
+        o, L = int(hb.out_off[i]), int(hb.lens[i])
+        sealed[o + L + (i % 16)] ^= 0x20  # flip a tag bit
+    src = torch.from_numpy(sealed).cuda()
+    pt = torch.zeros(hb.in_bytes, dtype=torch.uint8, device="cuda")
+    status = torch.zeros(hb.n, dtype=torch.uint8, device="cuda")
+    b = tg.make_batch(hb.n, src, pt, d["nonces"], aad=d["aad"], lens=d["lens"],
+                      in_off=d["out_off"], out_off=d["in_off"], aad_off=d["aad_off"],
+                      aad_len=d["aad_len"], key_idx=d.get("key_idx"), status=status)
+    tg.open_batch(key_obj, b)
+    torch.cuda.synchronize()
+    st = status.cpu().numpy()
+    back = pt.cpu().numpy()
+    for i in range(hb.n):
+        o, L = int(hb.in_off[i]), int(hb.lens[i])
+        if i in tamper:
+            assert st[i] == 0, i
+            assert not back[o:o + L].any(), "rejected record must be zeroed"
+        else:
+            assert st[i] == 1, i
+            assert np.array_equal(back[o:o + L], hb.inp[o:o + L]), ("open mismatch", i)
+
+
+LEN_MIX = [0, 1, 15, 16, 17, 31, 63, 64, 65, 100, 255, 256, 1000, 1024, 1025, 4096,
+           16383, 16384, 16385, 16400]
+
+
+@pytest.mark.parametrize("alg,klen", [("aesgcm", 16), ("aesgcm", 32), ("chacha", 32)])
+@pytest.mark.parametrize("align", [16, 1])
+def test_batch_ragged_vs_oracle(torch, tg, oracle_mod, alg, klen, align):
+    from batchpack import HostBatch
+    rng = np.random.default_rng(klen * 7 + align)
+    lens = LEN_MIX * 6 + list(rng.integers(0, 16401, 200))
+    hb = HostBatch(lens, payload_seed=align, align=align, aad_mode="random")
+    key = rng.bytes(klen)
+    obj = tg.HipAESGCM(bytearray(key)) if alg == "aesgcm" else tg.HipCHACHA20_POLY1305(bytearray(key))
+    _run_seal_open(torch, tg, oracle_mod, hb, alg, np.frombuffer(key, np.uint8), obj,
+                   tamper=(3, 17, 100))
+
+
+def test_chacha_key_table_vs_oracle(torch, tg, oracle_mod):
+    from batchpack import HostBatch
+    rng = np.random.default_rng(5)
+    lens = list(rng.integers(0, 4097, 700))
+    hb = HostBatch(lens, payload_seed=9, aad_mode="tls12", key_count=37)
+    keys = [rng.bytes(32) for _ in range(37)]
+    table = tg.KeyTable("chacha20-poly1305", keys)
+    karr = np.frombuffer(b"".join(keys), np.uint8).reshape(37, 32)
+    _run_seal_open(torch, tg, oracle_mod, hb, "chacha", karr, table, tamper=(1, 500))
+
+
+def test_record_batch_fixtures(torch, tg):
+    """The reference's own TLS 1.3 framed batches (tests/golden/record_batch.json)."""
+    from batchpack import HostBatch
+    for b in BATCH["batches"]:
+        recs = b["records"]
+        lens = [r["len"] for r in recs]
+        hb = HostBatch(lens, align=16, iv=H(b["iv"]))
+        for r in recs:
+            o = int(hb.in_off[r["seq"]])
+            hb.inp[o:o + r["len"]] = np.frombuffer(
+                bytes(detbytes("batch-pt-%s-%d" % (b["alg"], r["seq"]), r["len"])), np.uint8)
+        d = hb.to_device(torch)
+        key = bytearray(H(b["key"]))
+        obj = tg.HipCHACHA20_POLY1305(key) if b["alg"].startswith("chacha") else tg.HipAESGCM(key)
+        tg.seal_batch(obj, hb.batch_kwargs(d))
+        got = d["out"].cpu().numpy()
+        for i, r in enumerate(recs):
+            o, L = int(hb.out_off[i]), r["len"]
+            assert got[o + L:o + L + 16].tobytes().hex() == r["tag"], (b["alg"], i)
+            assert hashlib.sha256(got[o:o + L].tobytes()).hexdigest() == r["ct_sha256"]
+
+
+def test_make_nonces(torch, tg):
+    iv = detbytes("nonce-iv", 12)
+    out = torch.zeros(12 * 1000, dtype=torch.uint8, device="cuda")
+    tg.make_nonces(iv, 2 ** 40 - 7, 1000, out)
+    got = out.cpu().numpy().tobytes()
+    want = b"".join(bytes(tls13_nonce(iv, 2 ** 40 - 7 + i)) for i in range(1000))
+    assert got == want
+    tg.make_nonces(iv[:4], 5, 1000, out, tls13=False)
+    got = out.cpu().numpy().tobytes()
+    assert got == b"".join(bytes(iv[:4]) + (5 + i).to_bytes(8, "big") for i in range(1000))
+
+
+def test_config1_digest(torch, tg):
+    """BASELINE configs[0] through the device batch path: digest from the reference."""
+    from vectors import config1_inputs
+    key, iv, pts = config1_inputs()
+    n = len(pts)
+    inp = torch.from_numpy(np.frombuffer(b"".join(bytes(p) for p in pts), np.uint8).copy()).cuda()
+    out = torch.zeros(n * 1040, dtype=torch.uint8, device="cuda")
+    nonces = torch.zeros(12 * n, dtype=torch.uint8, device="cuda")
+    tg.make_nonces(iv, 0, n, nonces)
+    aad = torch.from_numpy(np.frombuffer(bytes(tls13_aad(1024)), np.uint8).copy()).cuda()
+    obj = tg.HipCHACHA20_POLY1305(key)
+    b = tg.make_batch(n, inp, out, nonces, aad=aad, fixed_len=1024, in_stride=1024,
+                      out_stride=1040, aad_stride=0, fixed_aad_len=5)
+    tg.seal_batch(obj, b)
+    torch.cuda.synchronize()
+    assert hashlib.sha256(out.cpu().numpy().tobytes()).hexdigest() == \
+        BATCH["config1"]["sealed_sha256"]
+
+
+# ------------------------------------------- full-size (BASELINE configs 2/3)
+
+@pytest.mark.parametrize("alg", ["aesgcm", "chacha"])
+def test_full_size_roundtrip_and_samples(torch, tg, oracle_mod, alg):
+    """2^20 x 16 KiB records: seal -> open round trip on the whole batch
+    (size-independent property), and 64 sampled records bit-exact vs the oracle."""
+    n, L = 1 << 20, 16384
+    g = torch.Generator(device="cuda").manual_seed(0x7715)
+    inp = torch.randint(0, 256, (n * L,), dtype=torch.uint8, device="cuda", generator=g)
+    key = bytes(detbytes("full-size-" + alg, 16 if alg == "aesgcm" else 32))
+    iv = detbytes("full-size-iv", 12)
+    obj = tg.HipAESGCM(bytearray(key)) if alg == "aesgcm" else tg.HipCHACHA20_POLY1305(bytearray(key))
+    nonces = torch.zeros(12 * n, dtype=torch.uint8, device="cuda")
+    tg.make_nonces(iv, 0, n, nonces)
+    aad = torch.tensor(list(tls13_aad(L)), dtype=torch.uint8, device="cuda")
+    sealed = torch.empty(n * (L + 16), dtype=torch.uint8, device="cuda")
+    tg.seal_batch(obj, tg.make_batch(n, inp, sealed, nonces, aad=aad, fixed_len=L, in_stride=L,
+                                     out_stride=L + 16, fixed_aad_len=5))
+    back = torch.empty_like(inp)
+    status = torch.zeros(n, dtype=torch.uint8, device="cuda")
+    tg.open_batch(obj, tg.make_batch(n, sealed, back, nonces, aad=aad, fixed_len=L,
+                                     in_stride=L + 16, out_stride=L, fixed_aad_len=5,
+                                     status=status))
+    torch.cuda.synchronize()
+    assert int(status.sum()) == n
+    assert torch.equal(back, inp)
+    rng = np.random.default_rng(1)
+    idx = np.unique(np.concatenate([[0, n - 1], rng.integers(0, n, 62)]))
+    for i in idx:
+        i = int(i)
+        pt = inp[i * L:(i + 1) * L].cpu().numpy().tobytes()
+        nonce = bytes(tls13_nonce(iv, i))
+        want = (oracle_mod.gcm_seal if alg == "aesgcm" else oracle_mod.chacha_seal)(
+            key, nonce, pt, bytes(tls13_aad(L)))
+        got = sealed[i * (L + 16):(i + 1) * (L + 16)].cpu().numpy().tobytes()
+        assert got == bytes(want), i
+    del inp, back, sealed
+    torch.cuda.empty_cache()

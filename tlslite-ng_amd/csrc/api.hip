@@ -1,0 +1,443 @@
+// api.hip -- the C ABI of libtlsgpu.so (declared in include/tlsgpu.h).
+//
+// Host side of the engine: key objects (AES key schedule and GHASH tables
+// built once per key, like AESGCM.__init__ at tlslite/utils/aesgcm.py:27-57),
+// the per-record drop-in entry points that the ctypes objects behind
+// tlsgpu.cipherfactory call for every record (recordlayer.py:558, :821), and
+// the device-pointer batch entry points.  No exceptions cross the ABI.
+#include <hip/hip_runtime.h>
+
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <string>
+
+#include "common.h"
+#include "tlsgpu.h"
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const char* fmt, ...) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof(buf), fmt, ap);
+    va_end(ap);
+    g_err = buf;
+    return code;
+}
+
+#define HIP_TRY(expr)                                                                 \
+    do {                                                                              \
+        hipError_t e_ = (expr);                                                       \
+        if (e_ != hipSuccess)                                                         \
+            return fail(TG_EHIP, "%s: %s (%s:%d)", #expr, hipGetErrorString(e_),      \
+                        __FILE__, __LINE__);                                          \
+    } while (0)
+
+// ---- host AES key schedule (FIPS-197 / rijndael.py:922-993) -------------
+struct HostAes {
+    uint8_t sbox[256];
+    HostAes() {
+        uint8_t exp[256], log[256];
+        uint8_t x = 1;
+        for (int i = 0; i < 255; ++i) {
+            exp[i] = x;
+            log[x] = (uint8_t)i;
+            x = (uint8_t)(x ^ xt(x));
+        }
+        for (int v = 0; v < 256; ++v) {
+            uint8_t inv = v ? exp[(255 - log[v]) % 255] : 0;
+            uint8_t s = inv, r = inv;
+            for (int k = 0; k < 4; ++k) {
+                r = (uint8_t)((r << 1) | (r >> 7));
+                s = (uint8_t)(s ^ r);
+            }
+            sbox[v] = (uint8_t)(s ^ 0x63);
+        }
+    }
+    static uint8_t xt(uint8_t a) { return (uint8_t)((a << 1) ^ ((a & 0x80) ? 0x1b : 0)); }
+
+    // round-key bytes, 16 * (rounds + 1)
+    int expand(const uint8_t* key, size_t keylen, uint8_t* rk) const {
+        const int nk = (int)keylen / 4, nr = nk + 6, total = 4 * (nr + 1);
+        memcpy(rk, key, keylen);
+        uint8_t rcon = 1;
+        for (int i = nk; i < total; ++i) {
+            uint8_t t[4];
+            memcpy(t, rk + 4 * (i - 1), 4);
+            if (i % nk == 0) {
+                uint8_t t0 = t[0];
+                t[0] = (uint8_t)(sbox[t[1]] ^ rcon);
+                t[1] = sbox[t[2]];
+                t[2] = sbox[t[3]];
+                t[3] = sbox[t0];
+                rcon = xt(rcon);
+            } else if (nk > 6 && i % nk == 4) {
+                for (int k = 0; k < 4; ++k) t[k] = sbox[t[k]];
+            }
+            for (int k = 0; k < 4; ++k) rk[4 * i + k] = (uint8_t)(rk[4 * (i - nk) + k] ^ t[k]);
+        }
+        return nr;
+    }
+
+    void encrypt(const uint8_t* rk, int nr, const uint8_t in[16], uint8_t out[16]) const {
+        uint8_t s[16], t[16];
+        for (int i = 0; i < 16; ++i) s[i] = (uint8_t)(in[i] ^ rk[i]);
+        for (int r = 1; r <= nr; ++r) {
+            for (int c = 0; c < 4; ++c)
+                for (int row = 0; row < 4; ++row) t[4 * c + row] = sbox[s[4 * ((c + row) & 3) + row]];
+            if (r != nr) {
+                for (int c = 0; c < 4; ++c) {
+                    uint8_t* a = t + 4 * c;
+                    uint8_t all = (uint8_t)(a[0] ^ a[1] ^ a[2] ^ a[3]), a0 = a[0];
+                    a[0] = (uint8_t)(a[0] ^ all ^ xt((uint8_t)(a[0] ^ a[1])));
+                    a[1] = (uint8_t)(a[1] ^ all ^ xt((uint8_t)(a[1] ^ a[2])));
+                    a[2] = (uint8_t)(a[2] ^ all ^ xt((uint8_t)(a[2] ^ a[3])));
+                    a[3] = (uint8_t)(a[3] ^ all ^ xt((uint8_t)(a[3] ^ a0)));
+                }
+            }
+            for (int i = 0; i < 16; ++i) s[i] = (uint8_t)(t[i] ^ rk[16 * r + i]);
+        }
+        memcpy(out, s, 16);
+    }
+};
+
+const HostAes& host_aes() {
+    static HostAes a;
+    return a;
+}
+
+uint32_t le32(const uint8_t* p) {
+    return (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16) | ((uint32_t)p[3] << 24);
+}
+
+// GHASH tables in the block byte layout.  A field element is the 16-byte
+// block read as a big-endian integer whose MSB is the x^0 coefficient
+// (aesgcm.py:8-14); multiplying by x is a right shift with the 0xe1 << 120
+// reduction (AESGCM._gcmShift, aesgcm.py:168-178).  V[n] = H * x^n, and
+// M_j[b] = XOR of V[8j + t] over the bits t (MSB first) set in b.
+void build_ghash_tables(const uint8_t h[16], uint4* table) {
+    uint64_t hi = 0, lo = 0;
+    for (int i = 0; i < 8; ++i) hi = (hi << 8) | h[i];
+    for (int i = 8; i < 16; ++i) lo = (lo << 8) | h[i];
+    uint64_t vhi[128], vlo[128];
+    for (int n = 0; n < 128; ++n) {
+        vhi[n] = hi;
+        vlo[n] = lo;
+        const uint64_t carry = lo & 1;
+        lo = (lo >> 1) | (hi << 63);
+        hi >>= 1;
+        if (carry) hi ^= 0xe1ull << 56;
+    }
+    for (int j = 0; j < 16; ++j) {
+        for (int b = 0; b < 256; ++b) {
+            uint64_t zh = 0, zl = 0;
+            for (int t = 0; t < 8; ++t) {
+                if (b & (0x80 >> t)) {
+                    zh ^= vhi[8 * j + t];
+                    zl ^= vlo[8 * j + t];
+                }
+            }
+            uint8_t bytes[16];
+            for (int k = 0; k < 8; ++k) {
+                bytes[k] = (uint8_t)(zh >> (56 - 8 * k));
+                bytes[8 + k] = (uint8_t)(zl >> (56 - 8 * k));
+            }
+            table[j * 256 + b] = make_uint4(le32(bytes), le32(bytes + 4), le32(bytes + 8),
+                                            le32(bytes + 12));
+        }
+    }
+}
+
+}  // namespace
+
+struct tg_key {
+    int alg;
+    size_t keylen;
+    size_t nkeys;
+    int device;
+    int rounds;
+    hipStream_t stream;
+    void* dev_key;          // GcmKeyDev (AES) or ChachaKeyDev[nkeys]
+    // staging for the per-record drop-in path
+    uint8_t* h_stage;
+    uint8_t* d_stage;
+    size_t stage_cap;
+};
+
+namespace {
+
+int select_device(const tg_key* k) {
+    int cur = -1;
+    HIP_TRY(hipGetDevice(&cur));
+    if (cur != k->device) HIP_TRY(hipSetDevice(k->device));
+    return TG_OK;
+}
+
+int ensure_stage(tg_key* k, size_t bytes) {
+    if (bytes <= k->stage_cap) return TG_OK;
+    size_t cap = k->stage_cap ? k->stage_cap : 65536;
+    while (cap < bytes) cap *= 2;
+    if (k->h_stage) (void)hipHostFree(k->h_stage);
+    if (k->d_stage) (void)hipFree(k->d_stage);
+    k->h_stage = nullptr;
+    k->d_stage = nullptr;
+    k->stage_cap = 0;
+    HIP_TRY(hipHostMalloc((void**)&k->h_stage, cap, hipHostMallocDefault));
+    HIP_TRY(hipMalloc((void**)&k->d_stage, cap));
+    k->stage_cap = cap;
+    return TG_OK;
+}
+
+int launch(tg_key* k, const tg_batch& b, bool open, hipStream_t s) {
+    if (k->alg == TG_AES_GCM)
+        return tg_launch_gcm(static_cast<const tg::GcmKeyDev*>(k->dev_key), k->rounds, b, open, s);
+    return tg_launch_chacha(static_cast<const tg::ChachaKeyDev*>(k->dev_key), b, open, s);
+}
+
+size_t align16(size_t v) { return (v + 15) & ~(size_t)15; }
+
+// One record through the staging buffers: [nonce | aad | input | output | status]
+int single(tg_key* k, const uint8_t* nonce, size_t noncelen, const uint8_t* aad, size_t aadlen,
+           const uint8_t* in, size_t inlen, uint8_t* out, bool open) {
+    if (!k) return fail(TG_EINVAL, "null key");
+    if (noncelen != 12) return fail(TG_ENONCE, "Bad nonce length");
+    if ((aadlen && !aad) || (inlen && !in)) return fail(TG_EINVAL, "null buffer");
+    if (open && inlen < 16) {   // aesgcm.py:135-136, chacha20_poly1305.py:76-77
+        return 0;
+    }
+    const size_t len = open ? inlen - 16 : inlen;
+    if (len > 0xffffffffull || aadlen > 0xffffffffull) return fail(TG_EINVAL, "record too long");
+    const size_t o_aad = 16, o_in = align16(o_aad + aadlen), o_out = align16(o_in + inlen);
+    const size_t outlen = open ? len : len + 16;
+    const size_t o_st = align16(o_out + outlen), total = o_st + 16;
+    int rc = select_device(k);
+    if (rc) return rc;
+    if ((rc = ensure_stage(k, total))) return rc;
+    memcpy(k->h_stage, nonce, 12);
+    if (aadlen) memcpy(k->h_stage + o_aad, aad, aadlen);
+    if (inlen) memcpy(k->h_stage + o_in, in, inlen);
+    HIP_TRY(hipMemcpyAsync(k->d_stage, k->h_stage, o_out, hipMemcpyHostToDevice, k->stream));
+    tg_batch b;
+    memset(&b, 0, sizeof(b));
+    b.n = 1;
+    b.in = k->d_stage + o_in;
+    b.fixed_len = (uint32_t)len;
+    b.fixed_aad_len = (uint32_t)aadlen;
+    b.out = k->d_stage + o_out;
+    b.nonce = k->d_stage;
+    b.aad = k->d_stage + o_aad;
+    b.status = open ? k->d_stage + o_st : nullptr;
+    if ((rc = launch(k, b, open, k->stream))) return fail(rc, "kernel launch failed");
+    HIP_TRY(hipMemcpyAsync(k->h_stage + o_out, k->d_stage + o_out, total - o_out,
+                           hipMemcpyDeviceToHost, k->stream));
+    HIP_TRY(hipStreamSynchronize(k->stream));
+    if (open) {
+        const int ok = k->h_stage[o_st] == 1;
+        if (ok && len) memcpy(out, k->h_stage + o_out, len);
+        if (!ok && len) memset(out, 0, len);
+        return ok;
+    }
+    memcpy(out, k->h_stage + o_out, outlen);
+    return TG_OK;
+}
+
+int batch(tg_key* k, const tg_batch* b, void* stream, bool open) {
+    if (!k || !b) return fail(TG_EINVAL, "null argument");
+    if (b->n == 0) return TG_OK;
+    if (!b->in || !b->out || !b->nonce) return fail(TG_EINVAL, "null device buffer");
+    if (!b->aad && (b->aad_len || b->fixed_aad_len)) return fail(TG_EINVAL, "null aad");
+    if (k->nkeys > 1 && !b->key_idx) return fail(TG_EINVAL, "key table needs key_idx");
+    if (k->alg == TG_AES_GCM && b->key_idx)
+        return fail(TG_EINVAL, "AES-GCM key tables are not supported yet");
+    int rc = select_device(k);
+    if (rc) return rc;
+    hipStream_t s = stream ? static_cast<hipStream_t>(stream) : k->stream;
+    if ((rc = launch(k, *b, open, s))) return fail(rc, "kernel launch failed: %s",
+                                                   hipGetErrorString(hipGetLastError()));
+    return TG_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* tg_version(void) { return "tlsgpu 0.1.0 (gfx950)"; }
+
+const char* tg_last_error(void) { return g_err.c_str(); }
+
+int tg_device_count(int* count) {
+    if (!count) return fail(TG_EINVAL, "null count");
+    int n = 0;
+    hipError_t e = hipGetDeviceCount(&n);
+    if (e != hipSuccess) {
+        *count = 0;
+        return fail(TG_ENODEV, "hipGetDeviceCount: %s", hipGetErrorString(e));
+    }
+    *count = n;
+    return TG_OK;
+}
+
+int tg_init(int device) {
+    int n = 0;
+    int rc = tg_device_count(&n);
+    if (rc) return rc;
+    if (device < 0 || device >= n) return fail(TG_ENODEV, "device %d not present (%d)", device, n);
+    HIP_TRY(hipSetDevice(device));
+    return TG_OK;
+}
+
+int tg_key_create(int alg, const uint8_t* keys, size_t keylen, size_t nkeys, tg_key** out) {
+    if (!out || !keys || nkeys == 0) return fail(TG_EINVAL, "null argument");
+    *out = nullptr;
+    if (alg == TG_AES_GCM) {
+        if (keylen != 16 && keylen != 32) return fail(TG_EKEYLEN, "AES-GCM key must be 16 or 32 bytes");
+        if (nkeys != 1) return fail(TG_EINVAL, "AES-GCM key tables are not supported yet");
+    } else if (alg == TG_CHACHA20_POLY1305) {
+        if (keylen != 32) return fail(TG_EKEYLEN, "Key must be 256 bit long");
+    } else {
+        return fail(TG_EINVAL, "unknown algorithm %d", alg);
+    }
+    int dev = 0;
+    HIP_TRY(hipGetDevice(&dev));
+    tg_key* k = new (std::nothrow) tg_key();
+    if (!k) return fail(TG_ENOMEM, "out of host memory");
+    k->alg = alg;
+    k->keylen = keylen;
+    k->nkeys = nkeys;
+    k->device = dev;
+    int rc = TG_OK;
+    hipError_t e = hipStreamCreateWithFlags(&k->stream, hipStreamNonBlocking);
+    if (e != hipSuccess) {
+        delete k;
+        return fail(TG_EHIP, "hipStreamCreate: %s", hipGetErrorString(e));
+    }
+    if (alg == TG_AES_GCM) {
+        tg::GcmKeyDev* hk = new (std::nothrow) tg::GcmKeyDev();
+        if (!hk) rc = fail(TG_ENOMEM, "out of host memory");
+        if (!rc) {
+            uint8_t rk[240];
+            const HostAes& aes = host_aes();
+            const int nr = aes.expand(keys, keylen, rk);
+            for (int w = 0; w < 4 * (nr + 1); ++w) hk->rk[w] = le32(rk + 4 * w);
+            hk->rounds = (uint32_t)nr;
+            k->rounds = nr;
+            uint8_t zero[16] = {0}, h[16];
+            aes.encrypt(rk, nr, zero, h);                     // H = E_K(0^128)
+            build_ghash_tables(h, hk->ghash);
+            e = hipMalloc(&k->dev_key, sizeof(tg::GcmKeyDev));
+            if (e == hipSuccess) e = hipMemcpy(k->dev_key, hk, sizeof(tg::GcmKeyDev), hipMemcpyHostToDevice);
+            if (e != hipSuccess) rc = fail(TG_EHIP, "key upload: %s", hipGetErrorString(e));
+            memset(rk, 0, sizeof(rk));
+            memset(hk, 0, sizeof(*hk));
+            delete hk;
+        }
+    } else {
+        tg::ChachaKeyDev* hk = new (std::nothrow) tg::ChachaKeyDev[nkeys];
+        if (!hk) rc = fail(TG_ENOMEM, "out of host memory");
+        if (!rc) {
+            for (size_t i = 0; i < nkeys; ++i)
+                for (int w = 0; w < 8; ++w) hk[i].k[w] = le32(keys + 32 * i + 4 * w);
+            const size_t bytes = sizeof(tg::ChachaKeyDev) * nkeys;
+            e = hipMalloc(&k->dev_key, bytes);
+            if (e == hipSuccess) e = hipMemcpy(k->dev_key, hk, bytes, hipMemcpyHostToDevice);
+            if (e != hipSuccess) rc = fail(TG_EHIP, "key upload: %s", hipGetErrorString(e));
+            memset(hk, 0, sizeof(tg::ChachaKeyDev) * nkeys);
+            delete[] hk;
+        }
+    }
+    if (rc) {
+        tg_key_destroy(k);
+        return rc;
+    }
+    *out = k;
+    return TG_OK;
+}
+
+int tg_key_destroy(tg_key* k) {
+    if (!k) return TG_OK;
+    int cur = -1;
+    if (hipGetDevice(&cur) == hipSuccess && cur != k->device) (void)hipSetDevice(k->device);
+    if (k->stream) (void)hipStreamSynchronize(k->stream);
+    if (k->dev_key) {
+        // scrub key material before release
+        size_t bytes = k->alg == TG_AES_GCM ? sizeof(tg::GcmKeyDev) : sizeof(tg::ChachaKeyDev) * k->nkeys;
+        (void)hipMemset(k->dev_key, 0, bytes);
+        (void)hipFree(k->dev_key);
+    }
+    if (k->h_stage) (void)hipHostFree(k->h_stage);
+    if (k->d_stage) (void)hipFree(k->d_stage);
+    if (k->stream) (void)hipStreamDestroy(k->stream);
+    if (cur >= 0 && cur != k->device) (void)hipSetDevice(cur);
+    delete k;
+    return TG_OK;
+}
+
+int tg_key_info(const tg_key* k, int* alg, size_t* keylen, size_t* nkeys) {
+    if (!k) return fail(TG_EINVAL, "null key");
+    if (alg) *alg = k->alg;
+    if (keylen) *keylen = k->keylen;
+    if (nkeys) *nkeys = k->nkeys;
+    return TG_OK;
+}
+
+int tg_seal(tg_key* k, const uint8_t* nonce, size_t noncelen, const uint8_t* aad, size_t aadlen,
+            const uint8_t* pt, size_t len, uint8_t* out) {
+    if (!out) return fail(TG_EINVAL, "null output");
+    return single(k, nonce, noncelen, aad, aadlen, pt, len, out, false);
+}
+
+int tg_open(tg_key* k, const uint8_t* nonce, size_t noncelen, const uint8_t* aad, size_t aadlen,
+            const uint8_t* in, size_t inlen, uint8_t* pt) {
+    if (!pt && inlen > 16) return fail(TG_EINVAL, "null output");
+    return single(k, nonce, noncelen, aad, aadlen, in, inlen, pt, true);
+}
+
+int tg_seal_batch(tg_key* k, const tg_batch* b, void* stream) { return batch(k, b, stream, false); }
+
+int tg_open_batch(tg_key* k, const tg_batch* b, void* stream) { return batch(k, b, stream, true); }
+
+int tg_make_nonces(int mode, const uint8_t* iv, size_t ivlen, uint64_t seq0, uint64_t n,
+                   uint8_t* out, void* stream) {
+    if (!iv || !out) return fail(TG_EINVAL, "null argument");
+    if (!((mode == 0 && ivlen == 12) || (mode == 1 && ivlen == 4)))
+        return fail(TG_EINVAL, "mode %d needs a %d-byte iv", mode, mode == 0 ? 12 : 4);
+    if (n == 0) return TG_OK;
+    int rc = tg_launch_nonces(mode, iv, seq0, n, out, static_cast<hipStream_t>(stream));
+    return rc ? fail(rc, "nonce kernel launch failed") : TG_OK;
+}
+
+int tg_malloc(void** p, size_t bytes) {
+    if (!p) return fail(TG_EINVAL, "null argument");
+    HIP_TRY(hipMalloc(p, bytes ? bytes : 1));
+    return TG_OK;
+}
+
+int tg_free(void* p) {
+    if (p) HIP_TRY(hipFree(p));
+    return TG_OK;
+}
+
+int tg_memcpy_h2d(void* dst, const void* src, size_t bytes, void* stream) {
+    if (!bytes) return TG_OK;
+    HIP_TRY(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, static_cast<hipStream_t>(stream)));
+    HIP_TRY(hipStreamSynchronize(static_cast<hipStream_t>(stream)));
+    return TG_OK;
+}
+
+int tg_memcpy_d2h(void* dst, const void* src, size_t bytes, void* stream) {
+    if (!bytes) return TG_OK;
+    HIP_TRY(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, static_cast<hipStream_t>(stream)));
+    HIP_TRY(hipStreamSynchronize(static_cast<hipStream_t>(stream)));
+    return TG_OK;
+}
+
+int tg_stream_sync(void* stream) {
+    HIP_TRY(hipStreamSynchronize(static_cast<hipStream_t>(stream)));
+    return TG_OK;
+}
+
+}  // extern "C"

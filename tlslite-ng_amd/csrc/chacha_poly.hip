@@ -1,0 +1,256 @@
+// chacha_poly.hip -- batched ChaCha20-Poly1305 seal/open for gfx950 (CDNA4).
+//
+// Restates CHACHA20_POLY1305.seal/open (tlslite/utils/chacha20_poly1305.py:
+// 48-94) over ChaCha (chacha.py:98-153) and Poly1305 (poly1305.py:32-48),
+// one TLS record per lane, pure 32-bit VALU work (no tables, no LDS):
+//
+//   * the one-time Poly1305 key is ChaCha block 0 (chacha20_poly1305.py:35-38),
+//     the payload uses blocks 1.. (chacha20_poly1305.py:58);
+//   * each 64-byte keystream block is XORed with four 16-byte loads and its
+//     four ciphertext blocks go straight into the Poly1305 accumulator, so
+//     mac_data = aad || pad || ct || pad || le64 || le64 (:60-63) is never
+//     materialised;
+//   * Poly1305 runs in five 26-bit limbs with 32x32->64 multiply-adds.
+#include "common.h"
+
+namespace tg {
+namespace {
+
+constexpr int kChachaThreads = 256;
+
+#define QR(a, b, c, d)                                  \
+    a += b; d ^= a; d = rotl32(d, 16);                  \
+    c += d; b ^= c; b = rotl32(b, 12);                  \
+    a += b; d ^= a; d = rotl32(d, 8);                   \
+    c += d; b ^= c; b = rotl32(b, 7);
+
+// ChaCha.chacha_block (chacha.py:98-109): 10 double rounds + feed-forward.
+__device__ __forceinline__ void chacha_block(const uint32_t (&k)[8], uint32_t ctr, uint32_t n0,
+                                             uint32_t n1, uint32_t n2, uint32_t (&o)[16]) {
+    uint32_t x0 = 0x61707865u, x1 = 0x3320646eu, x2 = 0x79622d32u, x3 = 0x6b206574u;
+    uint32_t x4 = k[0], x5 = k[1], x6 = k[2], x7 = k[3];
+    uint32_t x8 = k[4], x9 = k[5], x10 = k[6], x11 = k[7];
+    uint32_t x12 = ctr, x13 = n0, x14 = n1, x15 = n2;
+#pragma unroll
+    for (int r = 0; r < 10; ++r) {
+        QR(x0, x4, x8, x12);
+        QR(x1, x5, x9, x13);
+        QR(x2, x6, x10, x14);
+        QR(x3, x7, x11, x15);
+        QR(x0, x5, x10, x15);
+        QR(x1, x6, x11, x12);
+        QR(x2, x7, x8, x13);
+        QR(x3, x4, x9, x14);
+    }
+    o[0] = x0 + 0x61707865u; o[1] = x1 + 0x3320646eu;
+    o[2] = x2 + 0x79622d32u; o[3] = x3 + 0x6b206574u;
+    o[4] = x4 + k[0]; o[5] = x5 + k[1]; o[6] = x6 + k[2]; o[7] = x7 + k[3];
+    o[8] = x8 + k[4]; o[9] = x9 + k[5]; o[10] = x10 + k[6]; o[11] = x11 + k[7];
+    o[12] = x12 + ctr; o[13] = x13 + n0; o[14] = x14 + n1; o[15] = x15 + n2;
+}
+#undef QR
+
+// Poly1305 state in 26-bit limbs (value = sum h_i * 2^(26 i)).
+struct Poly {
+    uint32_t r0, r1, r2, r3, r4;
+    uint32_t s1, s2, s3, s4;  // 5 * r_i: 2^130 == 5 (mod 2^130 - 5)
+    uint32_t h0, h1, h2, h3, h4;
+    uint32_t p0, p1, p2, p3;  // s half of the one-time key
+};
+
+__device__ __forceinline__ void poly_init(Poly& p, const uint32_t (&otk)[16]) {
+    // r = LE(key[0:16]) & 0x0ffffffc0ffffffc0ffffffc0fffffff (poly1305.py:37-38)
+    p.r0 = otk[0] & 0x3ffffffu;
+    p.r1 = __builtin_amdgcn_alignbit(otk[1], otk[0], 26) & 0x3ffff03u;
+    p.r2 = __builtin_amdgcn_alignbit(otk[2], otk[1], 20) & 0x3ffc0ffu;
+    p.r3 = __builtin_amdgcn_alignbit(otk[3], otk[2], 14) & 0x3f03fffu;
+    p.r4 = (otk[3] >> 8) & 0x00fffffu;
+    p.s1 = p.r1 * 5; p.s2 = p.r2 * 5; p.s3 = p.r3 * 5; p.s4 = p.r4 * 5;
+    p.h0 = p.h1 = p.h2 = p.h3 = p.h4 = 0;
+    p.p0 = otk[4]; p.p1 = otk[5]; p.p2 = otk[6]; p.p3 = otk[7];
+}
+
+__device__ __forceinline__ uint64_t mul64(uint32_t a, uint32_t b) { return (uint64_t)a * b; }
+
+// acc = (acc + LE(m || 0x01)) * r mod 2^130-5 for one full 16-byte block
+// (poly1305.py:43-46).  mac_data is padded to 16 bytes (chacha20_poly1305.py:
+// 41-46), so every block carries the 2^128 bit.
+__device__ __forceinline__ void poly_block(Poly& p, uint4 m) {
+    const uint32_t M26 = 0x3ffffffu;
+    uint32_t h0 = p.h0 + (m.x & M26);
+    uint32_t h1 = p.h1 + (__builtin_amdgcn_alignbit(m.y, m.x, 26) & M26);
+    uint32_t h2 = p.h2 + (__builtin_amdgcn_alignbit(m.z, m.y, 20) & M26);
+    uint32_t h3 = p.h3 + (__builtin_amdgcn_alignbit(m.w, m.z, 14) & M26);
+    uint32_t h4 = p.h4 + ((m.w >> 8) | (1u << 24));
+    uint64_t d0 = mul64(h0, p.r0) + mul64(h1, p.s4) + mul64(h2, p.s3) + mul64(h3, p.s2) + mul64(h4, p.s1);
+    uint64_t d1 = mul64(h0, p.r1) + mul64(h1, p.r0) + mul64(h2, p.s4) + mul64(h3, p.s3) + mul64(h4, p.s2);
+    uint64_t d2 = mul64(h0, p.r2) + mul64(h1, p.r1) + mul64(h2, p.r0) + mul64(h3, p.s4) + mul64(h4, p.s3);
+    uint64_t d3 = mul64(h0, p.r3) + mul64(h1, p.r2) + mul64(h2, p.r1) + mul64(h3, p.r0) + mul64(h4, p.s4);
+    uint64_t d4 = mul64(h0, p.r4) + mul64(h1, p.r3) + mul64(h2, p.r2) + mul64(h3, p.r1) + mul64(h4, p.r0);
+    uint32_t c;
+    c = (uint32_t)(d0 >> 26); h0 = (uint32_t)d0 & M26;
+    d1 += c; c = (uint32_t)(d1 >> 26); h1 = (uint32_t)d1 & M26;
+    d2 += c; c = (uint32_t)(d2 >> 26); h2 = (uint32_t)d2 & M26;
+    d3 += c; c = (uint32_t)(d3 >> 26); h3 = (uint32_t)d3 & M26;
+    d4 += c; c = (uint32_t)(d4 >> 26); h4 = (uint32_t)d4 & M26;
+    h0 += c * 5; c = h0 >> 26; h0 &= M26;
+    h1 += c;
+    p.h0 = h0; p.h1 = h1; p.h2 = h2; p.h3 = h3; p.h4 = h4;
+}
+
+// tag = LE16((acc + s) mod 2^128) (poly1305.py:47-48)
+__device__ __forceinline__ uint4 poly_finish(const Poly& p) {
+    const uint32_t M26 = 0x3ffffffu;
+    uint32_t h0 = p.h0, h1 = p.h1, h2 = p.h2, h3 = p.h3, h4 = p.h4, c;
+    c = h1 >> 26; h1 &= M26; h2 += c;
+    c = h2 >> 26; h2 &= M26; h3 += c;
+    c = h3 >> 26; h3 &= M26; h4 += c;
+    c = h4 >> 26; h4 &= M26; h0 += c * 5;
+    c = h0 >> 26; h0 &= M26; h1 += c;
+    // g = h + 5 - 2^130; use g when h >= 2^130 - 5
+    uint32_t g0 = h0 + 5; c = g0 >> 26; g0 &= M26;
+    uint32_t g1 = h1 + c; c = g1 >> 26; g1 &= M26;
+    uint32_t g2 = h2 + c; c = g2 >> 26; g2 &= M26;
+    uint32_t g3 = h3 + c; c = g3 >> 26; g3 &= M26;
+    uint32_t g4 = h4 + c - (1u << 26);
+    uint32_t sel = (g4 >> 31) - 1u;  // all ones when no borrow
+    h0 = (h0 & ~sel) | (g0 & sel);
+    h1 = (h1 & ~sel) | (g1 & sel);
+    h2 = (h2 & ~sel) | (g2 & sel);
+    h3 = (h3 & ~sel) | (g3 & sel);
+    h4 = (h4 & ~sel) | (g4 & sel);
+    uint32_t w0 = h0 | (h1 << 26);
+    uint32_t w1 = (h1 >> 6) | (h2 << 20);
+    uint32_t w2 = (h2 >> 12) | (h3 << 14);
+    uint32_t w3 = (h3 >> 18) | (h4 << 8);
+    uint64_t f = (uint64_t)w0 + p.p0;
+    w0 = (uint32_t)f;
+    f = (uint64_t)w1 + p.p1 + (f >> 32); w1 = (uint32_t)f;
+    f = (uint64_t)w2 + p.p2 + (f >> 32); w2 = (uint32_t)f;
+    f = (uint64_t)w3 + p.p3 + (f >> 32); w3 = (uint32_t)f;
+    return make_uint4(w0, w1, w2, w3);
+}
+
+template <bool OPEN, bool MULTIKEY>
+__global__ __launch_bounds__(kChachaThreads) void chacha_kernel(
+    const ChachaKeyDev* __restrict__ keys, tg_batch b) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= b.n) return;
+    uint32_t k[8];
+    const ChachaKeyDev* kp = keys + (MULTIKEY ? b.key_idx[i] : 0);
+#pragma unroll
+    for (int w = 0; w < 8; ++w) k[w] = kp->k[w];
+
+    const uint8_t* in = rec_in(b, i);
+    uint8_t* out = rec_out(b, i);
+    const uint32_t len = rec_len(b, i);
+    const uint8_t* ad = rec_aad(b, i);
+    const uint32_t alen = rec_aad_len(b, i);
+    const bool aligned = (((uintptr_t)in | (uintptr_t)out) & 15) == 0;
+    const uint4 nv = load_partial(b.nonce + 12 * i, 12);
+
+    uint32_t ks[16];
+    chacha_block(k, 0, nv.x, nv.y, nv.z, ks);  // poly1305_key_gen
+    Poly p;
+    poly_init(p, ks);
+
+    for (uint32_t off = 0; off < alen; off += 16) {
+        uint32_t m = alen - off < 16 ? alen - off : 16;
+        poly_block(p, load_partial(ad + off, m));
+    }
+
+    const uint32_t nfull = len >> 6;
+    uint32_t j = 0;
+    for (; j < nfull; ++j) {
+        chacha_block(k, j + 1, nv.x, nv.y, nv.z, ks);
+        uint4 d[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) d[q] = load16(in + 64 * j + 16 * q, aligned);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            uint4 c = make_uint4(d[q].x ^ ks[4 * q], d[q].y ^ ks[4 * q + 1], d[q].z ^ ks[4 * q + 2],
+                                 d[q].w ^ ks[4 * q + 3]);
+            store16(out + 64 * j + 16 * q, c, aligned);
+            poly_block(p, OPEN ? d[q] : c);
+        }
+    }
+    const uint32_t rem = len - 64 * nfull;
+    if (rem) {
+        chacha_block(k, nfull + 1, nv.x, nv.y, nv.z, ks);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            if (16u * q < rem) {
+                uint32_t m = rem - 16 * q < 16 ? rem - 16 * q : 16;
+                uint4 d = load_partial(in + 64 * nfull + 16 * q, m);
+                uint4 c = mask_tail(make_uint4(d.x ^ ks[4 * q], d.y ^ ks[4 * q + 1],
+                                               d.z ^ ks[4 * q + 2], d.w ^ ks[4 * q + 3]), m);
+                store_partial(out + 64 * nfull + 16 * q, c, m);
+                poly_block(p, OPEN ? d : c);
+            }
+        }
+    }
+    // le64(len(aad)) || le64(len(ct))
+    poly_block(p, make_uint4(alen, 0, len, 0));
+    const uint4 tag = poly_finish(p);
+    const bool tag_aligned = aligned && (len & 15) == 0;
+    if (!OPEN) {
+        store16(out + len, tag, tag_aligned);
+        return;
+    }
+    const uint4 exp = load16(in + len, tag_aligned);
+    const uint32_t diff = (exp.x ^ tag.x) | (exp.y ^ tag.y) | (exp.z ^ tag.z) | (exp.w ^ tag.w);
+    if (b.status) b.status[i] = diff == 0;
+    if (diff) {
+        const uint4 z = make_uint4(0, 0, 0, 0);
+        for (uint32_t q = 0; q < (len >> 4); ++q) store16(out + 16 * q, z, aligned);
+        if (len & 15) store_partial(out + (len & ~15u), z, len & 15);
+    }
+}
+
+template <bool OPEN, bool MULTIKEY>
+int launch(const ChachaKeyDev* keys, const tg_batch& b, hipStream_t s) {
+    const uint64_t blocks = (b.n + kChachaThreads - 1) / kChachaThreads;
+    hipLaunchKernelGGL((chacha_kernel<OPEN, MULTIKEY>), dim3((unsigned)blocks),
+                       dim3(kChachaThreads), 0, s, keys, b);
+    return hipGetLastError() == hipSuccess ? TG_OK : TG_EHIP;
+}
+
+// RecordLayer._getNonce (recordlayer.py:522-534) for a run of sequence numbers.
+__global__ void nonce_kernel(int mode, uint4 iv, uint64_t seq0, uint64_t n, uint8_t* out) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint64_t seq = seq0 + i;
+    const uint32_t hi = bswap32((uint32_t)(seq >> 32)), lo = bswap32((uint32_t)seq);
+    uint32_t w0, w1, w2;
+    if (mode == 0) {          // iv12 xor (0^4 || be64(seq))
+        w0 = iv.x; w1 = iv.y ^ hi; w2 = iv.z ^ lo;
+    } else {                  // iv4 || be64(seq)
+        w0 = iv.x; w1 = hi; w2 = lo;
+    }
+    uint32_t* o = reinterpret_cast<uint32_t*>(out + 12 * i);
+    if ((((uintptr_t)out) & 3) == 0) {
+        o[0] = w0; o[1] = w1; o[2] = w2;
+    } else {
+        store_partial(out + 12 * i, make_uint4(w0, w1, w2, 0), 12);
+    }
+}
+
+}  // namespace
+}  // namespace tg
+
+int tg_launch_chacha(const tg::ChachaKeyDev* keys, const tg_batch& b, bool open, hipStream_t s) {
+    const bool multi = b.key_idx != nullptr;
+    if (open) return multi ? tg::launch<true, true>(keys, b, s) : tg::launch<true, false>(keys, b, s);
+    return multi ? tg::launch<false, true>(keys, b, s) : tg::launch<false, false>(keys, b, s);
+}
+
+int tg_launch_nonces(int mode, const uint8_t* iv_host, uint64_t seq0, uint64_t n, uint8_t* out,
+                     hipStream_t s) {
+    uint32_t w[3] = {0, 0, 0};
+    const int ivlen = mode == 0 ? 12 : 4;
+    for (int k = 0; k < ivlen; ++k) w[k >> 2] |= (uint32_t)iv_host[k] << (8 * (k & 3));
+    const uint64_t blocks = (n + 255) / 256;
+    hipLaunchKernelGGL(tg::nonce_kernel, dim3((unsigned)blocks), dim3(256), 0, s, mode,
+                       make_uint4(w[0], w[1], w[2], 0), seq0, n, out);
+    return hipGetLastError() == hipSuccess ? TG_OK : TG_EHIP;
+}

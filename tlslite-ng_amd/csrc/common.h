@@ -1,0 +1,104 @@
+// common.h -- shared device helpers and key layouts for libtlsgpu.
+//
+// Layout of one AES-GCM key in HBM (GcmKeyDev) and the per-record accessors
+// used by every kernel.  All record data is handled as little-endian 32-bit
+// words of the wire bytes, so a 16-byte block is one uint4 load and no byte
+// swapping happens on the hot path (GHASH tables are built in the same byte
+// layout on the host, see api.cpp).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "tlsgpu.h"
+
+namespace tg {
+
+// 16 tables x 256 entries x 16 bytes: M_j[b] = b * x^(8j) * H, so that
+// X * H = XOR_j M_j[byte_j(X)] (GCM bit order, aesgcm.py:8-14).
+constexpr int kGhashEntries = 16 * 256;
+
+struct GcmKeyDev {
+    uint32_t rk[60];       // round keys as LE words of the key-schedule bytes
+    uint32_t rounds;       // 10 (AES-128) or 14 (AES-256)
+    uint32_t pad[3];
+    uint4 ghash[kGhashEntries];
+};
+
+struct ChachaKeyDev {
+    uint32_t k[8];         // key as LE words (chacha.py:101, _bytearray_to_words)
+};
+
+__device__ __forceinline__ uint4 xor4(uint4 a, uint4 b) {
+    return make_uint4(a.x ^ b.x, a.y ^ b.y, a.z ^ b.z, a.w ^ b.w);
+}
+
+__device__ __forceinline__ uint32_t rotl32(uint32_t v, int c) {
+    return __builtin_amdgcn_alignbit(v, v, 32 - c);
+}
+
+__device__ __forceinline__ uint32_t bswap32(uint32_t v) {
+    return __builtin_bswap32(v);
+}
+
+__device__ __forceinline__ const uint8_t* rec_in(const tg_batch& b, uint64_t i) {
+    return b.in + (b.in_off ? b.in_off[i] : i * b.in_stride);
+}
+__device__ __forceinline__ uint8_t* rec_out(const tg_batch& b, uint64_t i) {
+    return b.out + (b.out_off ? b.out_off[i] : i * b.out_stride);
+}
+__device__ __forceinline__ uint32_t rec_len(const tg_batch& b, uint64_t i) {
+    return b.len ? b.len[i] : b.fixed_len;
+}
+__device__ __forceinline__ const uint8_t* rec_aad(const tg_batch& b, uint64_t i) {
+    return b.aad + (b.aad_off ? b.aad_off[i] : i * b.aad_stride);
+}
+__device__ __forceinline__ uint32_t rec_aad_len(const tg_batch& b, uint64_t i) {
+    return b.aad_len ? b.aad_len[i] : b.fixed_aad_len;
+}
+
+// n (<= 16) bytes from p, zero-padded, as 4 LE words.
+__device__ __forceinline__ uint4 load_partial(const uint8_t* p, uint32_t n) {
+    uint32_t w[4] = {0, 0, 0, 0};
+    for (uint32_t k = 0; k < n; ++k) w[k >> 2] |= (uint32_t)p[k] << (8 * (k & 3));
+    return make_uint4(w[0], w[1], w[2], w[3]);
+}
+
+__device__ __forceinline__ void store_partial(uint8_t* p, uint4 v, uint32_t n) {
+    uint32_t w[4] = {v.x, v.y, v.z, v.w};
+    for (uint32_t k = 0; k < n; ++k) p[k] = (uint8_t)(w[k >> 2] >> (8 * (k & 3)));
+}
+
+// Full 16-byte block; the vector form when the record is 16-byte aligned.
+__device__ __forceinline__ uint4 load16(const uint8_t* p, bool aligned) {
+    if (aligned) return *reinterpret_cast<const uint4*>(p);
+    return load_partial(p, 16);
+}
+
+__device__ __forceinline__ void store16(uint8_t* p, uint4 v, bool aligned) {
+    if (aligned) {
+        *reinterpret_cast<uint4*>(p) = v;
+    } else {
+        store_partial(p, v, 16);
+    }
+}
+
+__device__ __forceinline__ uint4 mask_tail(uint4 v, uint32_t n) {
+    // keep the first n (< 16) bytes of a block, zero the rest
+    uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        int keep = (int)n - 4 * k;
+        uint32_t m = keep >= 4 ? 0xffffffffu : (keep <= 0 ? 0u : ((1u << (8 * keep)) - 1u));
+        w[k] &= m;
+    }
+    return make_uint4(w[0], w[1], w[2], w[3]);
+}
+
+}  // namespace tg
+
+// Launchers implemented in the kernel files (host side).
+int tg_launch_gcm(const tg::GcmKeyDev* key, int rounds, const tg_batch& b, bool open,
+                  hipStream_t s);
+int tg_launch_chacha(const tg::ChachaKeyDev* keys, const tg_batch& b, bool open, hipStream_t s);
+int tg_launch_nonces(int mode, const uint8_t* iv_host, uint64_t seq0, uint64_t n, uint8_t* out,
+                     hipStream_t s);

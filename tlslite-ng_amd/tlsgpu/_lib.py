@@ -1,0 +1,111 @@
+"""ctypes binding of libtlsgpu.so (include/tlsgpu.h).
+
+The product path.  There is no fallback: if the HIP library is missing or no
+GPU is visible, the calls raise -- nothing here routes through a CPU
+implementation.
+"""
+import ctypes
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libtlsgpu.so")
+
+TG_OK = 0
+TG_EINVAL = -22
+TG_EKEYLEN = -2
+TG_ENONCE = -3
+TG_ENOMEM = -12
+TG_EHIP = -5
+TG_ENODEV = -19
+
+TG_AES_GCM = 0
+TG_CHACHA20_POLY1305 = 1
+
+# Every function include/tlsgpu.h declares (checked by tests/test_abi.py).
+EXPORTS = ("tg_version", "tg_last_error", "tg_device_count", "tg_init", "tg_key_create",
+           "tg_key_destroy", "tg_key_info", "tg_seal", "tg_open", "tg_seal_batch",
+           "tg_open_batch", "tg_make_nonces", "tg_malloc", "tg_free", "tg_memcpy_h2d",
+           "tg_memcpy_d2h", "tg_stream_sync")
+
+
+class TgBatch(ctypes.Structure):
+    """``struct tg_batch`` (include/tlsgpu.h)."""
+    _fields_ = [
+        ("n", ctypes.c_uint64),
+        ("inp", ctypes.c_void_p),
+        ("in_off", ctypes.c_void_p),
+        ("in_stride", ctypes.c_uint64),
+        ("len", ctypes.c_void_p),
+        ("fixed_len", ctypes.c_uint32),
+        ("fixed_aad_len", ctypes.c_uint32),
+        ("out", ctypes.c_void_p),
+        ("out_off", ctypes.c_void_p),
+        ("out_stride", ctypes.c_uint64),
+        ("nonce", ctypes.c_void_p),
+        ("aad", ctypes.c_void_p),
+        ("aad_off", ctypes.c_void_p),
+        ("aad_stride", ctypes.c_uint64),
+        ("aad_len", ctypes.c_void_p),
+        ("key_idx", ctypes.c_void_p),
+        ("status", ctypes.c_void_p),
+    ]
+
+
+class TlsGpuError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__("libtlsgpu error %d: %s" % (code, msg))
+        self.code = code
+
+
+_lib = None
+
+
+def load():
+    """Load libtlsgpu.so (raises OSError if it has not been built)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise OSError("libtlsgpu.so not built (run __graft_entry__.build() or "
+                      "make -C tlslite-ng_amd/csrc): %s" % LIB_PATH)
+    l = ctypes.CDLL(LIB_PATH)
+    p, sz, i, u64 = ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int, ctypes.c_uint64
+    l.tg_version.restype = ctypes.c_char_p
+    l.tg_version.argtypes = []
+    l.tg_last_error.restype = ctypes.c_char_p
+    l.tg_last_error.argtypes = []
+    l.tg_device_count.argtypes = [ctypes.POINTER(ctypes.c_int)]
+    l.tg_init.argtypes = [i]
+    l.tg_key_create.argtypes = [i, p, sz, sz, ctypes.POINTER(ctypes.c_void_p)]
+    l.tg_key_destroy.argtypes = [p]
+    l.tg_key_info.argtypes = [p, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(sz),
+                              ctypes.POINTER(sz)]
+    l.tg_seal.argtypes = [p, p, sz, p, sz, p, sz, p]
+    l.tg_open.argtypes = [p, p, sz, p, sz, p, sz, p]
+    l.tg_seal_batch.argtypes = [p, ctypes.POINTER(TgBatch), p]
+    l.tg_open_batch.argtypes = [p, ctypes.POINTER(TgBatch), p]
+    l.tg_make_nonces.argtypes = [i, p, sz, u64, u64, p, p]
+    l.tg_malloc.argtypes = [ctypes.POINTER(ctypes.c_void_p), sz]
+    l.tg_free.argtypes = [p]
+    l.tg_memcpy_h2d.argtypes = [p, p, sz, p]
+    l.tg_memcpy_d2h.argtypes = [p, p, sz, p]
+    l.tg_stream_sync.argtypes = [p]
+    for name in EXPORTS:
+        if name not in ("tg_version", "tg_last_error"):
+            getattr(l, name).restype = ctypes.c_int
+    _lib = l
+    return l
+
+
+def check(rc):
+    """Raise TlsGpuError for a negative status, return rc otherwise."""
+    if rc < 0:
+        msg = load().tg_last_error()
+        raise TlsGpuError(rc, msg.decode() if msg else "")
+    return rc
+
+
+def device_count():
+    n = ctypes.c_int(0)
+    rc = load().tg_device_count(ctypes.byref(n))
+    return n.value if rc == 0 else 0
