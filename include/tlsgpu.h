@@ -16,7 +16,7 @@
  * current when it was created and is not thread-safe (one handle per
  * connection direction, as ConnectionState.encContext is in the reference,
  * recordlayer.py:239-249).  Batch entry points take DEVICE pointers and are
- * ordered on the given HIP stream (NULL = the handle's own stream).
+ * ordered on the given HIP stream (NULL = the null stream).
  */
 #ifndef TLSGPU_H
 #define TLSGPU_H

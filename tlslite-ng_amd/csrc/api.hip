@@ -255,7 +255,7 @@ int batch(tg_key* k, const tg_batch* b, void* stream, bool open) {
         return fail(TG_EINVAL, "AES-GCM key tables are not supported yet");
     int rc = select_device(k);
     if (rc) return rc;
-    hipStream_t s = stream ? static_cast<hipStream_t>(stream) : k->stream;
+    hipStream_t s = static_cast<hipStream_t>(stream);  // NULL = the null stream
     if ((rc = launch(k, *b, open, s))) return fail(rc, "kernel launch failed: %s",
                                                    hipGetErrorString(hipGetLastError()));
     return TG_OK;

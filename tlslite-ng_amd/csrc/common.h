@@ -56,16 +56,21 @@ __device__ __forceinline__ uint32_t rec_aad_len(const tg_batch& b, uint64_t i) {
     return b.aad_len ? b.aad_len[i] : b.fixed_aad_len;
 }
 
-// n (<= 16) bytes from p, zero-padded, as 4 LE words.
+// n (<= 16) bytes from p, zero-padded, as 4 LE words.  Fully unrolled with
+// compile-time word indices so nothing is placed in scratch.
 __device__ __forceinline__ uint4 load_partial(const uint8_t* p, uint32_t n) {
     uint32_t w[4] = {0, 0, 0, 0};
-    for (uint32_t k = 0; k < n; ++k) w[k >> 2] |= (uint32_t)p[k] << (8 * (k & 3));
+#pragma unroll
+    for (uint32_t k = 0; k < 16; ++k)
+        if (k < n) w[k >> 2] |= (uint32_t)p[k] << (8 * (k & 3));
     return make_uint4(w[0], w[1], w[2], w[3]);
 }
 
 __device__ __forceinline__ void store_partial(uint8_t* p, uint4 v, uint32_t n) {
-    uint32_t w[4] = {v.x, v.y, v.z, v.w};
-    for (uint32_t k = 0; k < n; ++k) p[k] = (uint8_t)(w[k >> 2] >> (8 * (k & 3)));
+    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (uint32_t k = 0; k < 16; ++k)
+        if (k < n) p[k] = (uint8_t)(w[k >> 2] >> (8 * (k & 3)));
 }
 
 // Full 16-byte block; the vector form when the record is 16-byte aligned.
