@@ -1,0 +1,42 @@
+"""Run each AEAD kernel once on a fixed batch, for rocprofv3 counter passes.
+
+    rocprofv3 --pmc <counters> --output-format csv -d out -- python tools/prof_kernels.py
+"""
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+for p in (ROOT, os.path.join(ROOT, "tlslite-ng_amd"), os.path.join(ROOT, "tests", "golden")):
+    sys.path.insert(0, p)
+
+import torch  # noqa: E402
+import tlsgpu  # noqa: E402
+from vectors import tls13_aad  # noqa: E402
+
+
+def main():
+    n = int(os.environ.get("PROF_RECORDS", 1 << 18))
+    L = int(os.environ.get("PROF_LEN", 16384))
+    algs = os.environ.get("PROF_ALGS", "aes128gcm,chacha20-poly1305").split(",")
+    inp = torch.randint(0, 256, (n * L,), dtype=torch.uint8, device="cuda")
+    sealed = torch.empty(n * (L + 16), dtype=torch.uint8, device="cuda")
+    back = torch.empty_like(inp)
+    status = torch.zeros(n, dtype=torch.uint8, device="cuda")
+    nonces = torch.empty(12 * n, dtype=torch.uint8, device="cuda")
+    tlsgpu.make_nonces(bytes(12), 0, n, nonces)
+    aad = torch.tensor(list(tls13_aad(L)), dtype=torch.uint8, device="cuda")
+    for a in algs:
+        c = tlsgpu.HipAESGCM(bytearray(16)) if a == "aes128gcm" else \
+            tlsgpu.HipCHACHA20_POLY1305(bytearray(32))
+        tlsgpu.seal_batch(c, tlsgpu.make_batch(n, inp, sealed, nonces, aad=aad, fixed_len=L,
+                                               in_stride=L, out_stride=L + 16, fixed_aad_len=5))
+        tlsgpu.open_batch(c, tlsgpu.make_batch(n, sealed, back, nonces, aad=aad, fixed_len=L,
+                                               in_stride=L + 16, out_stride=L, fixed_aad_len=5,
+                                               status=status))
+        torch.cuda.synchronize()
+        assert int(status.sum()) == n
+    print("prof_kernels done", n, L, algs)
+
+
+if __name__ == "__main__":
+    main()
