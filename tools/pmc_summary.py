@@ -1,0 +1,35 @@
+"""Summarise tools/pmc.sh output: one row per kernel, counters summed over dispatches."""
+import csv
+import glob
+import os
+import sys
+from collections import defaultdict
+
+
+def short(name):
+    for k in ("gcm_kernel<10, false>", "gcm_kernel<10, true>", "gcm_kernel<14, false>",
+              "gcm_kernel<14, true>", "chacha_kernel<false, false>", "chacha_kernel<true, false>",
+              "chacha_kernel<false, true>", "chacha_kernel<true, true>"):
+        if k in name:
+            return k
+    return None
+
+
+def main(d):
+    vals = defaultdict(lambda: defaultdict(float))
+    disp = defaultdict(set)
+    for f in glob.glob(os.path.join(d, "p*", "**", "*counter_collection.csv"), recursive=True):
+        for row in csv.DictReader(open(f)):
+            k = short(row.get("Kernel_Name", ""))
+            if not k:
+                continue
+            vals[k][row["Counter_Name"]] += float(row["Counter_Value"])
+            disp[k].add(row.get("Dispatch_Id"))
+    for k, v in vals.items():
+        print("==", k, "dispatches:", len(disp[k]))
+        for c in sorted(v):
+            print("   %-34s %16.4g" % (c, v[c]))
+
+
+if __name__ == "__main__":
+    main(sys.argv[1] if len(sys.argv) > 1 else "gpurun_out/pmc")
