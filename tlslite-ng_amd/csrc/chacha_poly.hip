@@ -131,6 +131,37 @@ __device__ __forceinline__ uint4 poly_finish(const Poly& p) {
     return make_uint4(w0, w1, w2, w3);
 }
 
+// The 64-byte blocks of a record: keystream block j+1 XOR payload, with the
+// next block's payload loaded one iteration ahead (the load of block j+1 is in
+// flight while block j's 20 rounds run).  ALIGNED records use 16-byte vector
+// loads and stores with no per-access branches.
+template <bool OPEN, bool ALIGNED>
+__device__ __forceinline__ void full_blocks(const uint32_t (&k)[8], uint4 nv, const uint8_t* in,
+                                            uint8_t* out, uint32_t nfull, Poly& p) {
+    if (nfull == 0) return;
+    uint4 d[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) d[q] = load16(in + 16 * q, ALIGNED);
+    for (uint32_t j = 0; j < nfull; ++j) {
+        // prefetch block j+1 (the last iteration re-reads its own block: in bounds)
+        const uint32_t jn = j + 1 < nfull ? j + 1 : j;
+        uint4 nx[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) nx[q] = load16(in + 64 * jn + 16 * q, ALIGNED);
+        uint32_t ks[16];
+        chacha_block(k, j + 1, nv.x, nv.y, nv.z, ks);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            uint4 c = make_uint4(d[q].x ^ ks[4 * q], d[q].y ^ ks[4 * q + 1], d[q].z ^ ks[4 * q + 2],
+                                 d[q].w ^ ks[4 * q + 3]);
+            store16(out + 64 * j + 16 * q, c, ALIGNED);
+            poly_block(p, OPEN ? d[q] : c);
+        }
+#pragma unroll
+        for (int q = 0; q < 4; ++q) d[q] = nx[q];
+    }
+}
+
 template <bool OPEN, bool MULTIKEY>
 __global__ __launch_bounds__(kChachaThreads) void chacha_kernel(
     const ChachaKeyDev* __restrict__ keys, tg_batch b) {
@@ -149,10 +180,12 @@ __global__ __launch_bounds__(kChachaThreads) void chacha_kernel(
     const bool aligned = (((uintptr_t)in | (uintptr_t)out) & 15) == 0;
     const uint4 nv = load_partial(b.nonce + 12 * i, 12);
 
-    uint32_t ks[16];
-    chacha_block(k, 0, nv.x, nv.y, nv.z, ks);  // poly1305_key_gen
     Poly p;
-    poly_init(p, ks);
+    {
+        uint32_t otk[16];
+        chacha_block(k, 0, nv.x, nv.y, nv.z, otk);  // poly1305_key_gen
+        poly_init(p, otk);
+    }
 
     for (uint32_t off = 0; off < alen; off += 16) {
         uint32_t m = alen - off < 16 ? alen - off : 16;
@@ -160,20 +193,12 @@ __global__ __launch_bounds__(kChachaThreads) void chacha_kernel(
     }
 
     const uint32_t nfull = len >> 6;
-    uint32_t j = 0;
-    for (; j < nfull; ++j) {
-        chacha_block(k, j + 1, nv.x, nv.y, nv.z, ks);
-        uint4 d[4];
-#pragma unroll
-        for (int q = 0; q < 4; ++q) d[q] = load16(in + 64 * j + 16 * q, aligned);
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            uint4 c = make_uint4(d[q].x ^ ks[4 * q], d[q].y ^ ks[4 * q + 1], d[q].z ^ ks[4 * q + 2],
-                                 d[q].w ^ ks[4 * q + 3]);
-            store16(out + 64 * j + 16 * q, c, aligned);
-            poly_block(p, OPEN ? d[q] : c);
-        }
+    if (aligned) {
+        full_blocks<OPEN, true>(k, nv, in, out, nfull, p);
+    } else {
+        full_blocks<OPEN, false>(k, nv, in, out, nfull, p);
     }
+    uint32_t ks[16];
     const uint32_t rem = len - 64 * nfull;
     if (rem) {
         chacha_block(k, nfull + 1, nv.x, nv.y, nv.z, ks);

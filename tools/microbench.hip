@@ -54,6 +54,11 @@ OP_KERNEL(k_mul_hi_u32, uint32_t, c + seed + threadIdx.x, ASM2("v_mul_hi_u32"))
 OP_KERNEL(k_fma_f32, float, c + seed + threadIdx.x, ASM3("v_fma_f32"))
 OP_KERNEL(k_pk_fma_f32, double, c + seed + threadIdx.x, ASM3("v_pk_fma_f32"))
 OP_KERNEL(k_fma_f64, double, c + seed + threadIdx.x, ASM3("v_fma_f64"))
+OP_KERNEL(k_bitop3, uint32_t, c + seed + threadIdx.x, asm volatile("v_bitop3_b32 %0, %0, %1, %2 bitop3:0x96" : "+v"(x[c]) : "v"(N1), "v"(N2)))
+OP_KERNEL(k_xor_sdwa, uint32_t, c + seed + threadIdx.x, asm volatile("v_xor_b32_sdwa %0, %0, %1 dst_sel:WORD_0 dst_unused:UNUSED_PRESERVE src0_sel:WORD_1 src1_sel:WORD_1" : "+v"(x[c]) : "v"(N1)))
+OP_KERNEL(k_lshrrev, uint32_t, c + seed + threadIdx.x, ASM2("v_lshrrev_b32"))
+OP_KERNEL(k_and_b32, uint32_t, c + seed + threadIdx.x, ASM2("v_and_b32"))
+OP_KERNEL(k_xad_u32, uint32_t, c + seed + threadIdx.x, ASM3("v_xad_u32"))
 OP_KERNEL(k_add_u64, uint64_t, c + seed + threadIdx.x, asm volatile("v_lshl_add_u64 %0, %0, 0, %1" : "+v"(x[c]) : "v"(N1)))
 
 __global__ void k_mad_u64_u32(uint64_t* out, uint32_t seed) {
@@ -68,6 +73,29 @@ __global__ void k_mad_u64_u32(uint64_t* out, uint32_t seed) {
     for (int c = 0; c < CH; ++c) acc += x[c];
     out[blockIdx.x * blockDim.x + threadIdx.x] = acc;
 }
+
+#define QR(a, b, c, d)                                              \
+    a += b; d ^= a; d = __builtin_amdgcn_alignbit(d, d, 16);        \
+    c += d; b ^= c; b = __builtin_amdgcn_alignbit(b, b, 20);        \
+    a += b; d ^= a; d = __builtin_amdgcn_alignbit(d, d, 24);        \
+    c += d; b ^= c; b = __builtin_amdgcn_alignbit(b, b, 25);
+__global__ void k_chacha_only(uint32_t* out, uint32_t seed) {
+    uint32_t acc = 0;
+    const uint32_t k0 = seed, k1 = seed * 3, k2 = seed * 5, k3 = seed * 7;
+    for (int blk = 0; blk < 64; ++blk) {
+        uint32_t x0 = 0x61707865u, x1 = 0x3320646eu, x2 = 0x79622d32u, x3 = 0x6b206574u;
+        uint32_t x4 = k0, x5 = k1, x6 = k2, x7 = k3, x8 = k0 ^ 1, x9 = k1 ^ 1, x10 = k2 ^ 1, x11 = k3 ^ 1;
+        uint32_t x12 = blk, x13 = threadIdx.x, x14 = blockIdx.x, x15 = seed;
+#pragma unroll
+        for (int r = 0; r < 10; ++r) {
+            QR(x0, x4, x8, x12); QR(x1, x5, x9, x13); QR(x2, x6, x10, x14); QR(x3, x7, x11, x15);
+            QR(x0, x5, x10, x15); QR(x1, x6, x11, x12); QR(x2, x7, x8, x13); QR(x3, x4, x9, x14);
+        }
+        acc ^= x0 ^ x1 ^ x2 ^ x3 ^ x4 ^ x5 ^ x6 ^ x7 ^ x8 ^ x9 ^ x10 ^ x11 ^ x12 ^ x13 ^ x14 ^ x15;
+    }
+    out[blockIdx.x * blockDim.x + threadIdx.x] = acc;
+}
+#undef QR
 
 // LDS random-lookup rate: T-table style, per-lane replicated (conflict-free)
 // vs shared random (conflicted), and 16-byte entries (ds_read_b128).
@@ -172,6 +200,18 @@ int main() {
     RUN(k_mul_hi_u32, uint32_t);
     RUN(k_mad_u64_u32, uint64_t);
     RUN(k_add_u64, uint64_t);
+    RUN(k_bitop3, uint32_t);
+    RUN(k_xor_sdwa, uint32_t);
+    RUN(k_lshrrev, uint32_t);
+    RUN(k_and_b32, uint32_t);
+    RUN(k_xad_u32, uint32_t);
+    // ChaCha20 block function alone (no memory), 4 and 8 waves per SIMD
+    for (int bs : {256, 512, 1024}) {
+        float ms = time_kernel(k_chacha_only, dim3(cus * 4), dim3(bs), (uint32_t*)buf, 7u);
+        double blocks = (double)cus * 4 * bs * 64;
+        printf("chacha-only blockDim %4d %8.3f ms  %6.2f CU-clk/block (@2.4GHz)  %7.1f GB/s keystream\n",
+               bs, ms, (ms / 1e3) * 2.4e9 * cus / blocks, blocks * 64 / (ms / 1e3) / 1e9);
+    }
     RUN(k_fma_f32, float);
     RUN(k_pk_fma_f32, double);
     RUN(k_fma_f64, double);
