@@ -4,13 +4,17 @@
 // keystream of Python_AES_CTR (python_aes.py:101-116) and the Rijndael round
 // (rijndael.py:995-1038), one TLS record per lane:
 //
-//   * the AES round is a T-table round; Te0 (1 KiB) is replicated 64x in LDS
-//     so lane l always reads its own bank (ds_read_b32 is conflict-free) and
-//     each lookup address is one v_perm_b32; Te1..Te3 are byte rotations of
-//     Te0 (v_alignbit), the final round's S-box byte is byte 1 of Te0[x].
+//   * the AES round is a T-table round over Te0 and Te2 = rotl16(Te0), each
+//     replicated 32x in LDS so lane l always reads bank l%32 (ds_read_b32 is
+//     conflict-free); a column needs one rotation (v_alignbit) instead of
+//     three; each lookup address is one v_perm_b32 or one full-rate bitop3;
+//     the final round's S-box byte is byte 1 of Te0[x].
+//   * counter mode: round 1 is cached per record (only the counter word
+//     changes between blocks), so it costs 4 lookups instead of 16.
 //   * GHASH multiplies by H with sixteen 8-bit tables M_j[b] = b*x^(8j)*H
 //     (64 KiB, staged into LDS once per workgroup): X*H = XOR_j M_j[X_j],
-//     i.e. 16 ds_read_b128 per block, no shifts and no reduction steps.
+//     i.e. 16 ds_read_b128 per block, no shifts and no reduction steps;
+//     3-input XORs are single full-rate v_bitop3_b32.
 //   * round keys are wave-uniform (single key per launch) and live in SGPRs.
 //
 // Counter blocks are nonce || be32(2 + j); the reference's 128-bit
@@ -57,104 +61,173 @@ constexpr TeTable make_te() {
 
 __constant__ TeTable c_te = make_te();
 
-constexpr int kGcmThreads = 1024;
-// LDS map (one workgroup per CU):
-//   [0, 64 KiB)        GHASH tables M_j[b] (16 x 256 x 16 B)
-//   [64 KiB, 128 KiB)  Te0, one copy per lane: entry x for lane l at
-//                      64 KiB + x * 256 + l * 4, so every lane reads its own
-//                      bank (ds_read_b32 conflict-free) and the byte address
-//                      is assembled by ONE v_perm_b32 from the state word.
+// LDS map (one workgroup per CU, no static LDS so the dynamic block is at 0):
+//   [0, 64 KiB)        GHASH tables, row b (256 B) = {M_0[b], ..., M_15[b]}:
+//                      entry (j, b) at b * 256 + j * 16
+//   [64 KiB, 128 KiB)  Te0 and Te2 = rotl16(Te0), row x (256 B) =
+//                      {Te0[x] x 32 copies, Te2[x] x 32 copies}; lane l reads
+//                      copy l % 32, i.e. bank l % 32 (conflict-free ds_read_b32)
+//   A round column then needs one rotation instead of three:
+//     Te0[a] ^ rotl8(Te0[b]) ^ rotl16(Te0[c]) ^ rotl24(Te0[d])
+//       = Te0[a] ^ Te2[c] ^ rotl8(Te0[b] ^ Te2[d]).
 constexpr uint32_t kTeBase = 65536;
 constexpr size_t kGcmLds = 2 * 65536;
 
 extern __shared__ __attribute__((aligned(16))) uint4 g_lds[];
 
-// The kernel declares no static LDS, so the dynamic block starts at LDS
-// address 0 and table addresses are absolute: the perm/shift result is the
-// ds_read address itself (constant parts go in the instruction's offset).
 #if defined(__HIP_DEVICE_COMPILE__)
 typedef const __attribute__((address_space(3))) uint32_t* lds_u32_ptr;
 typedef const __attribute__((address_space(3))) uint4* lds_u128_ptr;
 __device__ __forceinline__ uint32_t lds_u32(uint32_t addr) { return *(lds_u32_ptr)(uintptr_t)addr; }
 __device__ __forceinline__ uint4 lds_u128(uint32_t addr) { return *(lds_u128_ptr)(uintptr_t)addr; }
+__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
+    return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
+}
+__device__ __forceinline__ uint32_t and_or(uint32_t a, uint32_t b, uint32_t c) {  // (a & b) | c
+    return __builtin_amdgcn_bitop3_b32(a, b, c, 0xEA);
+}
 #else
 __device__ __forceinline__ uint32_t lds_u32(uint32_t) { return 0; }
 __device__ __forceinline__ uint4 lds_u128(uint32_t) { return uint4(); }
+__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) { return a ^ b ^ c; }
+__device__ __forceinline__ uint32_t and_or(uint32_t a, uint32_t b, uint32_t c) { return (a & b) | c; }
 #endif
 
-// Te0[byte K of x] for this lane; lane4 = {lane * 4, 0, 1, 0} (bytes 0..3).
-template <int K>
-__device__ __forceinline__ uint32_t TE(uint32_t x, uint32_t lane4) {
-    return lds_u32(__builtin_amdgcn_perm(x, lane4, 0x0c020000u | ((4u + K) << 8)));
+__device__ __forceinline__ uint4 xor4_3(uint4 a, uint4 b, uint4 c) {
+    return make_uint4(xor3(a.x, b.x, c.x), xor3(a.y, b.y, c.y), xor3(a.z, b.z, c.z),
+                      xor3(a.w, b.w, c.w));
 }
+
+// Byte address of row (byte K of x) for this lane; lane4 = 0x10000 | (lane%32)*4.
+template <int K>
+__device__ __forceinline__ uint32_t te_addr(uint32_t x, uint32_t lane4) {
+    if (K == 1) return and_or(x, 0xff00u, lane4);   // one full-rate bitop3
+    return __builtin_amdgcn_perm(x, lane4, 0x0c020000u | ((4u + K) << 8));
+}
+template <int K>
+__device__ __forceinline__ uint32_t T0(uint32_t x, uint32_t lane4) { return lds_u32(te_addr<K>(x, lane4)); }
+template <int K>
+__device__ __forceinline__ uint32_t T2(uint32_t x, uint32_t lane4) { return lds_u32(te_addr<K>(x, lane4) + 128); }
+
+// One T-table round column: rows from s_a byte 0, s_b byte 1, s_c byte 2, s_d byte 3.
+__device__ __forceinline__ uint32_t col(uint32_t sa, uint32_t sb, uint32_t sc, uint32_t sd,
+                                        uint32_t rk, uint32_t lane4) {
+    return xor3(T0<0>(sa, lane4), T2<2>(sc, lane4), rk) ^
+           rotl32(T0<1>(sb, lane4) ^ T2<3>(sd, lane4), 8);
+}
+
+// Final round column: S(x) is byte 1 of Te0[x].
+__device__ __forceinline__ uint32_t col_last(uint32_t sa, uint32_t sb, uint32_t sc, uint32_t sd,
+                                             uint32_t rk, uint32_t lane4) {
+    const uint32_t lo = __builtin_amdgcn_perm(T0<1>(sb, lane4), T0<0>(sa, lane4), 0x0c0c0501u);
+    const uint32_t hi = __builtin_amdgcn_perm(T0<3>(sd, lane4), T0<2>(sc, lane4), 0x05010c0cu);
+    return xor3(lo, hi, rk);
+}
+
+// Per-record round-1 constants for counter mode: after AddRoundKey the state
+// words s0..s2 (nonce ^ rk0) are the same for every block of the record, so
+// each round-1 column is a constant K_c XOR the one term that reads s3.
+struct CtrCache {
+    uint32_t k0, k1, k2, k3;
+};
 
 template <int NR>
-__device__ __forceinline__ uint4 aes_enc(uint32_t lane4, const uint32_t (&rk)[4 * (NR + 1)],
-                                         uint32_t i0, uint32_t i1, uint32_t i2, uint32_t i3) {
-    uint32_t s0 = i0 ^ rk[0], s1 = i1 ^ rk[1], s2 = i2 ^ rk[2], s3 = i3 ^ rk[3];
+__device__ __forceinline__ CtrCache ctr_cache(uint32_t lane4, const uint32_t (&rk)[4 * (NR + 1)],
+                                              uint4 nv) {
+    const uint32_t s0 = nv.x ^ rk[0], s1 = nv.y ^ rk[1], s2 = nv.z ^ rk[2];
+    CtrCache c;
+    // column 0: a=s0.b0 b=s1.b1 c=s2.b2 d=s3.b3(varies)
+    c.k0 = T0<0>(s0, lane4) ^ T2<2>(s2, lane4) ^ rotl32(T0<1>(s1, lane4), 8) ^ rk[4];
+    // column 1: a=s1.b0 b=s2.b1 c=s3.b2(varies) d=s0.b3
+    c.k1 = T0<0>(s1, lane4) ^ rotl32(T0<1>(s2, lane4) ^ T2<3>(s0, lane4), 8) ^ rk[5];
+    // column 2: a=s2.b0 b=s3.b1(varies) c=s0.b2 d=s1.b3
+    c.k2 = T0<0>(s2, lane4) ^ T2<2>(s0, lane4) ^ rotl32(T2<3>(s1, lane4), 8) ^ rk[6];
+    // column 3: a=s3.b0(varies) b=s0.b1 c=s1.b2 d=s2.b3
+    c.k3 = T2<2>(s1, lane4) ^ rotl32(T0<1>(s0, lane4) ^ T2<3>(s2, lane4), 8) ^ rk[7];
+    return c;
+}
+
+// E_K(nonce || be32(ctr)) using the round-1 cache.
+template <int NR>
+__device__ __forceinline__ uint4 aes_ctr(uint32_t lane4, const uint32_t (&rk)[4 * (NR + 1)],
+                                         const CtrCache& cc, uint32_t ctr) {
+    uint32_t s3 = bswap32(ctr) ^ rk[3];
+    uint32_t s0 = cc.k0 ^ rotl32(T2<3>(s3, lane4), 8);
+    uint32_t s1 = cc.k1 ^ T2<2>(s3, lane4);
+    uint32_t s2 = cc.k2 ^ rotl32(T0<1>(s3, lane4), 8);
+    uint32_t t3 = cc.k3 ^ T0<0>(s3, lane4);
+    uint32_t t0, t1, t2;
+    s3 = t3;
 #pragma unroll
-    for (int r = 1; r < NR; ++r) {
-        uint32_t t0 = TE<0>(s0, lane4) ^ rotl32(TE<1>(s1, lane4), 8) ^
-                      rotl32(TE<2>(s2, lane4), 16) ^ rotl32(TE<3>(s3, lane4), 24) ^ rk[4 * r];
-        uint32_t t1 = TE<0>(s1, lane4) ^ rotl32(TE<1>(s2, lane4), 8) ^
-                      rotl32(TE<2>(s3, lane4), 16) ^ rotl32(TE<3>(s0, lane4), 24) ^ rk[4 * r + 1];
-        uint32_t t2 = TE<0>(s2, lane4) ^ rotl32(TE<1>(s3, lane4), 8) ^
-                      rotl32(TE<2>(s0, lane4), 16) ^ rotl32(TE<3>(s1, lane4), 24) ^ rk[4 * r + 2];
-        uint32_t t3 = TE<0>(s3, lane4) ^ rotl32(TE<1>(s0, lane4), 8) ^
-                      rotl32(TE<2>(s1, lane4), 16) ^ rotl32(TE<3>(s2, lane4), 24) ^ rk[4 * r + 3];
+    for (int r = 2; r < NR; ++r) {
+        t0 = col(s0, s1, s2, s3, rk[4 * r], lane4);
+        t1 = col(s1, s2, s3, s0, rk[4 * r + 1], lane4);
+        t2 = col(s2, s3, s0, s1, rk[4 * r + 2], lane4);
+        t3 = col(s3, s0, s1, s2, rk[4 * r + 3], lane4);
         s0 = t0; s1 = t1; s2 = t2; s3 = t3;
     }
-    // final round: SubBytes + ShiftRows + AddRoundKey; S(x) is byte 1 of Te0[x],
-    // gathered from four lookups with two v_perm_b32 and an OR.
-#define SBW(a, b, c, d)                                                                  \
-    (__builtin_amdgcn_perm(TE<1>(b, lane4), TE<0>(a, lane4), 0x0c0c0501u) |                \
-     __builtin_amdgcn_perm(TE<3>(d, lane4), TE<2>(c, lane4), 0x05010c0cu))
-    const uint32_t o0 = SBW(s0, s1, s2, s3), o1 = SBW(s1, s2, s3, s0);
-    const uint32_t o2 = SBW(s2, s3, s0, s1), o3 = SBW(s3, s0, s1, s2);
-#undef SBW
-    return make_uint4(o0 ^ rk[4 * NR], o1 ^ rk[4 * NR + 1], o2 ^ rk[4 * NR + 2], o3 ^ rk[4 * NR + 3]);
+    return make_uint4(col_last(s0, s1, s2, s3, rk[4 * NR], lane4),
+                      col_last(s1, s2, s3, s0, rk[4 * NR + 1], lane4),
+                      col_last(s2, s3, s0, s1, rk[4 * NR + 2], lane4),
+                      col_last(s3, s0, s1, s2, rk[4 * NR + 3], lane4));
 }
 
-// y * H with the sixteen 8-bit tables (byte j of the block = byte j%4 of word
-// j/4): entry (j, b) at LDS byte j * 4096 + b * 16.
+// y * H with the sixteen 8-bit tables: X * H = XOR_j M_j[byte j of X]; byte j
+// of the block is byte j%4 of word j/4.  Row addresses b * 256 come from
+// full-rate ops (16-bit shift / AND), table j is the ds_read offset j * 16.
 __device__ __forceinline__ uint4 gmul(uint4 y) {
     const uint32_t w[4] = {y.x, y.y, y.z, y.w};
-    uint4 z = make_uint4(0, 0, 0, 0);
+    uint4 e[16];
 #pragma unroll
-    for (int j = 0; j < 16; ++j) {
-        const uint32_t v = w[j >> 2];
-        const int sh = 8 * (j & 3) - 4;
-        const uint32_t off = (sh < 0 ? (v << 4) : (v >> sh)) & 0xff0u;
-        z = xor4(z, lds_u128(off + 4096u * j));
+    for (int q = 0; q < 4; ++q) {
+        const uint32_t v = w[q], hi = v >> 16;
+        const uint32_t a0 = (uint32_t)(uint16_t)(v << 8);
+        const uint32_t a1 = v & 0xff00u;
+        const uint32_t a2 = (uint32_t)(uint16_t)(hi << 8);
+        const uint32_t a3 = hi & 0xff00u;
+        e[4 * q + 0] = lds_u128(a0 + 16 * (4 * q + 0));
+        e[4 * q + 1] = lds_u128(a1 + 16 * (4 * q + 1));
+        e[4 * q + 2] = lds_u128(a2 + 16 * (4 * q + 2));
+        e[4 * q + 3] = lds_u128(a3 + 16 * (4 * q + 3));
     }
-    return z;
+    uint4 z = xor4_3(e[0], e[1], e[2]);
+    z = xor4_3(z, e[3], e[4]);
+    z = xor4_3(z, e[5], e[6]);
+    z = xor4_3(z, e[7], e[8]);
+    z = xor4_3(z, e[9], e[10]);
+    z = xor4_3(z, e[11], e[12]);
+    z = xor4_3(z, e[13], e[14]);
+    return xor4(z, e[15]);
 }
 
-// Blocks [0, G*ngroups) of a record in groups of G (16*G bytes), the next
-// group's payload loaded one iteration ahead.
+// Full 16-byte blocks [0, G*ngroups) in groups of G.  The keystream of group
+// g+1 and the payload of group g+1 are produced while group g is XORed and
+// hashed, so the GHASH chain of seal (which needs the ciphertext) overlaps the
+// next group's AES rounds.
 template <int NR, bool OPEN, bool ALIGNED, int G>
 __device__ __forceinline__ uint4 ctr_groups(uint32_t lane4, const uint32_t (&rk)[4 * (NR + 1)],
-                                            uint4 nv, const uint8_t* in, uint8_t* out,
+                                            const CtrCache& cc, const uint8_t* in, uint8_t* out,
                                             uint32_t ngroups, uint4 y) {
     if (ngroups == 0) return y;
-    uint4 d[G];
+    uint4 d[G], ks[G];
 #pragma unroll
     for (int q = 0; q < G; ++q) d[q] = load16(in + 16 * q, ALIGNED);
+#pragma unroll
+    for (int q = 0; q < G; ++q) ks[q] = aes_ctr<NR>(lane4, rk, cc, 2u + q);
     for (uint32_t g = 0; g < ngroups; ++g) {
         const uint32_t gn = g + 1 < ngroups ? g + 1 : g;
-        uint4 nx[G];
+        uint4 nx[G], c[G];
 #pragma unroll
         for (int q = 0; q < G; ++q) nx[q] = load16(in + 16 * (G * gn + q), ALIGNED);
-        uint4 ks[G];
-#pragma unroll
-        for (int q = 0; q < G; ++q)
-            ks[q] = aes_enc<NR>(lane4, rk, nv.x, nv.y, nv.z, bswap32(2u + G * g + q));
 #pragma unroll
         for (int q = 0; q < G; ++q) {
-            const uint4 c = xor4(d[q], ks[q]);
-            store16(out + 16 * (G * g + q), c, ALIGNED);
-            y = gmul(xor4(y, OPEN ? d[q] : c));
+            c[q] = xor4(d[q], ks[q]);
+            store16(out + 16 * (G * g + q), c[q], ALIGNED);
         }
+#pragma unroll
+        for (int q = 0; q < G; ++q) ks[q] = aes_ctr<NR>(lane4, rk, cc, 2u + G * (g + 1) + q);
+#pragma unroll
+        for (int q = 0; q < G; ++q) y = gmul(xor4(y, OPEN ? d[q] : c[q]));
 #pragma unroll
         for (int q = 0; q < G; ++q) d[q] = nx[q];
     }
@@ -165,11 +238,15 @@ template <int NR, bool OPEN, int G, int THREADS>
 __global__ __launch_bounds__(THREADS) void gcm_kernel(const GcmKeyDev* __restrict__ key,
                                                       tg_batch b) {
     uint4* lds = g_lds;
-    // stage the GHASH tables and the per-lane Te0 copies
-    for (int e = threadIdx.x; e < kGhashEntries; e += blockDim.x) lds[e] = key->ghash[e];
+    // stage the GHASH rows (entry (j, b) -> b * 16 + j) and the Te0/Te2 copies
+    for (int e = threadIdx.x; e < kGhashEntries; e += blockDim.x)
+        lds[(e & 255) * 16 + (e >> 8)] = key->ghash[e];
     {
         uint32_t* te = reinterpret_cast<uint32_t*>(lds) + kTeBase / 4;
-        for (int e = threadIdx.x; e < 256 * 64; e += blockDim.x) te[e] = c_te.te0[e >> 6];
+        for (int e = threadIdx.x; e < 256 * 64; e += blockDim.x) {
+            const uint32_t v = c_te.te0[e >> 6];
+            te[e] = (e & 32) ? rotl32(v, 16) : v;
+        }
     }
     uint32_t rk[4 * (NR + 1)];
 #pragma unroll
@@ -178,7 +255,7 @@ __global__ __launch_bounds__(THREADS) void gcm_kernel(const GcmKeyDev* __restric
 
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= b.n) return;
-    const uint32_t lane4 = ((threadIdx.x & 63u) << 2) | 0x00010000u;
+    const uint32_t lane4 = ((threadIdx.x & 31u) << 2) | kTeBase;
 
     const uint8_t* in = rec_in(b, i);
     uint8_t* out = rec_out(b, i);
@@ -187,9 +264,10 @@ __global__ __launch_bounds__(THREADS) void gcm_kernel(const GcmKeyDev* __restric
     const uint32_t alen = rec_aad_len(b, i);
     const bool aligned = (((uintptr_t)in | (uintptr_t)out) & 15) == 0;
 
-    // J0 = nonce || be32(1): the tag mask (aesgcm.py:112-115)
     const uint4 nv = load_partial(b.nonce + 12 * i, 12);
-    const uint4 mask = aes_enc<NR>(lane4, rk, nv.x, nv.y, nv.z, bswap32(1u));
+    const CtrCache cc = ctr_cache<NR>(lane4, rk, nv);
+    // J0 = nonce || be32(1): the tag mask (aesgcm.py:112-115)
+    const uint4 mask = aes_ctr<NR>(lane4, rk, cc, 1u);
 
     // GHASH over the AAD, zero-padded (aesgcm.py:69-79)
     uint4 y = make_uint4(0, 0, 0, 0);
@@ -202,17 +280,17 @@ __global__ __launch_bounds__(THREADS) void gcm_kernel(const GcmKeyDev* __restric
     const uint32_t nfull = len >> 4;
     const uint32_t tail = len & 15;
     const uint32_t ngroups = nfull / G;
-    y = aligned ? ctr_groups<NR, OPEN, true, G>(lane4, rk, nv, in, out, ngroups, y)
-                : ctr_groups<NR, OPEN, false, G>(lane4, rk, nv, in, out, ngroups, y);
+    y = aligned ? ctr_groups<NR, OPEN, true, G>(lane4, rk, cc, in, out, ngroups, y)
+                : ctr_groups<NR, OPEN, false, G>(lane4, rk, cc, in, out, ngroups, y);
     for (uint32_t j = G * ngroups; j < nfull; ++j) {
-        const uint4 ks = aes_enc<NR>(lane4, rk, nv.x, nv.y, nv.z, bswap32(2u + j));
+        const uint4 ks = aes_ctr<NR>(lane4, rk, cc, 2u + j);
         const uint4 d = load16(in + 16 * j, aligned);
         const uint4 c = xor4(d, ks);
         store16(out + 16 * j, c, aligned);
         y = gmul(xor4(y, OPEN ? d : c));
     }
     if (tail) {
-        const uint4 ks = aes_enc<NR>(lane4, rk, nv.x, nv.y, nv.z, bswap32(2u + nfull));
+        const uint4 ks = aes_ctr<NR>(lane4, rk, cc, 2u + nfull);
         const uint4 d = load_partial(in + 16 * nfull, tail);
         const uint4 c = mask_tail(xor4(d, ks), tail);
         store_partial(out + 16 * nfull, c, tail);

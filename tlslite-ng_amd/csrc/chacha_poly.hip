@@ -131,13 +131,17 @@ __device__ __forceinline__ uint4 poly_finish(const Poly& p) {
     return make_uint4(w0, w1, w2, w3);
 }
 
-// The 64-byte blocks of a record: keystream block j+1 XOR payload, with the
-// next block's payload loaded one iteration ahead (the load of block j+1 is in
-// flight while block j's 20 rounds run).  ALIGNED records use 16-byte vector
-// loads and stores with no per-access branches.
+// The 64-byte blocks of a record.  Software-pipelined one block deep: while
+// block j is XORed and fed to Poly1305, the keystream of block j+1 is
+// generated and the payload of block j+1 is in flight, so seal's Poly1305
+// chain (which needs the ciphertext) overlaps the next block's 20 rounds.
+// Leaves in ks the keystream of block nfull+1 (the partial tail, if any).
+// ALIGNED records use 16-byte vector loads and stores with no branches.
 template <bool OPEN, bool ALIGNED>
 __device__ __forceinline__ void full_blocks(const uint32_t (&k)[8], uint4 nv, const uint8_t* in,
-                                            uint8_t* out, uint32_t nfull, Poly& p) {
+                                            uint8_t* out, uint32_t nfull, Poly& p,
+                                            uint32_t (&ks)[16]) {
+    chacha_block(k, 1, nv.x, nv.y, nv.z, ks);
     if (nfull == 0) return;
     uint4 d[4];
 #pragma unroll
@@ -145,18 +149,18 @@ __device__ __forceinline__ void full_blocks(const uint32_t (&k)[8], uint4 nv, co
     for (uint32_t j = 0; j < nfull; ++j) {
         // prefetch block j+1 (the last iteration re-reads its own block: in bounds)
         const uint32_t jn = j + 1 < nfull ? j + 1 : j;
-        uint4 nx[4];
+        uint4 nx[4], c[4];
 #pragma unroll
         for (int q = 0; q < 4; ++q) nx[q] = load16(in + 64 * jn + 16 * q, ALIGNED);
-        uint32_t ks[16];
-        chacha_block(k, j + 1, nv.x, nv.y, nv.z, ks);
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
-            uint4 c = make_uint4(d[q].x ^ ks[4 * q], d[q].y ^ ks[4 * q + 1], d[q].z ^ ks[4 * q + 2],
-                                 d[q].w ^ ks[4 * q + 3]);
-            store16(out + 64 * j + 16 * q, c, ALIGNED);
-            poly_block(p, OPEN ? d[q] : c);
+            c[q] = make_uint4(d[q].x ^ ks[4 * q], d[q].y ^ ks[4 * q + 1], d[q].z ^ ks[4 * q + 2],
+                              d[q].w ^ ks[4 * q + 3]);
+            store16(out + 64 * j + 16 * q, c[q], ALIGNED);
         }
+        chacha_block(k, j + 2, nv.x, nv.y, nv.z, ks);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) poly_block(p, OPEN ? d[q] : c[q]);
 #pragma unroll
         for (int q = 0; q < 4; ++q) d[q] = nx[q];
     }
@@ -193,15 +197,14 @@ __global__ __launch_bounds__(kChachaThreads) void chacha_kernel(
     }
 
     const uint32_t nfull = len >> 6;
-    if (aligned) {
-        full_blocks<OPEN, true>(k, nv, in, out, nfull, p);
-    } else {
-        full_blocks<OPEN, false>(k, nv, in, out, nfull, p);
-    }
     uint32_t ks[16];
+    if (aligned) {
+        full_blocks<OPEN, true>(k, nv, in, out, nfull, p, ks);
+    } else {
+        full_blocks<OPEN, false>(k, nv, in, out, nfull, p, ks);
+    }
     const uint32_t rem = len - 64 * nfull;
-    if (rem) {
-        chacha_block(k, nfull + 1, nv.x, nv.y, nv.z, ks);
+    if (rem) {  // ks already holds keystream block nfull + 1
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
             if (16u * q < rem) {
