@@ -62,8 +62,7 @@ constexpr TeTable make_te() {
 __constant__ TeTable c_te = make_te();
 
 // LDS map (one workgroup per CU, no static LDS so the dynamic block is at 0):
-//   [0, 64 KiB)        GHASH tables, row b (256 B) = {M_0[b], ..., M_15[b]}:
-//                      entry (j, b) at b * 256 + j * 16
+//   [0, 64 KiB)        GHASH tables, entry (j, b) = M_j[b] at j * 4096 + b * 16
 //   [64 KiB, 128 KiB)  Te0 and Te2 = rotl16(Te0), row x (256 B) =
 //                      {Te0[x] x 32 copies, Te2[x] x 32 copies}; lane l reads
 //                      copy l % 32, i.e. bank l % 32 (conflict-free ds_read_b32)
@@ -173,22 +172,19 @@ __device__ __forceinline__ uint4 aes_ctr(uint32_t lane4, const uint32_t (&rk)[4 
 }
 
 // y * H with the sixteen 8-bit tables: X * H = XOR_j M_j[byte j of X]; byte j
-// of the block is byte j%4 of word j/4.  Row addresses b * 256 come from
-// full-rate ops (16-bit shift / AND), table j is the ds_read offset j * 16.
+// of the block is byte j%4 of word j/4.  Entry (j, b) sits at j * 4096 + b * 16
+// (table j is the ds_read offset), so the 16 lanes of a ds_read_b128 group
+// land on the 16 bank slots by their own random bytes.
 __device__ __forceinline__ uint4 gmul(uint4 y) {
     const uint32_t w[4] = {y.x, y.y, y.z, y.w};
     uint4 e[16];
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
-        const uint32_t v = w[q], hi = v >> 16;
-        const uint32_t a0 = (uint32_t)(uint16_t)(v << 8);
-        const uint32_t a1 = v & 0xff00u;
-        const uint32_t a2 = (uint32_t)(uint16_t)(hi << 8);
-        const uint32_t a3 = hi & 0xff00u;
-        e[4 * q + 0] = lds_u128(a0 + 16 * (4 * q + 0));
-        e[4 * q + 1] = lds_u128(a1 + 16 * (4 * q + 1));
-        e[4 * q + 2] = lds_u128(a2 + 16 * (4 * q + 2));
-        e[4 * q + 3] = lds_u128(a3 + 16 * (4 * q + 3));
+        const uint32_t v = w[q];
+        e[4 * q + 0] = lds_u128(((v << 4) & 0xff0u) + 4096 * (4 * q + 0));
+        e[4 * q + 1] = lds_u128(((v >> 4) & 0xff0u) + 4096 * (4 * q + 1));
+        e[4 * q + 2] = lds_u128(((v >> 12) & 0xff0u) + 4096 * (4 * q + 2));
+        e[4 * q + 3] = lds_u128(((v >> 20) & 0xff0u) + 4096 * (4 * q + 3));
     }
     uint4 z = xor4_3(e[0], e[1], e[2]);
     z = xor4_3(z, e[3], e[4]);
@@ -238,9 +234,8 @@ template <int NR, bool OPEN, int G, int THREADS>
 __global__ __launch_bounds__(THREADS) void gcm_kernel(const GcmKeyDev* __restrict__ key,
                                                       tg_batch b) {
     uint4* lds = g_lds;
-    // stage the GHASH rows (entry (j, b) -> b * 16 + j) and the Te0/Te2 copies
-    for (int e = threadIdx.x; e < kGhashEntries; e += blockDim.x)
-        lds[(e & 255) * 16 + (e >> 8)] = key->ghash[e];
+    // stage the GHASH tables and the Te0/Te2 copies
+    for (int e = threadIdx.x; e < kGhashEntries; e += blockDim.x) lds[e] = key->ghash[e];
     {
         uint32_t* te = reinterpret_cast<uint32_t*>(lds) + kTeBase / 4;
         for (int e = threadIdx.x; e < 256 * 64; e += blockDim.x) {
