@@ -147,22 +147,22 @@ __device__ __forceinline__ void full_blocks(const uint32_t (&k)[8], uint4 nv, co
 #pragma unroll
     for (int q = 0; q < 4; ++q) d[q] = load16(in + 16 * q, ALIGNED);
     for (uint32_t j = 0; j < nfull; ++j) {
-        // prefetch block j+1 (the last iteration re-reads its own block: in bounds)
-        const uint32_t jn = j + 1 < nfull ? j + 1 : j;
-        uint4 nx[4], c[4];
-#pragma unroll
-        for (int q = 0; q < 4; ++q) nx[q] = load16(in + 64 * jn + 16 * q, ALIGNED);
+        // m = the Poly1305 input of block j (ciphertext: c for seal, d for open)
+        uint4 m[4];
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
-            c[q] = make_uint4(d[q].x ^ ks[4 * q], d[q].y ^ ks[4 * q + 1], d[q].z ^ ks[4 * q + 2],
-                              d[q].w ^ ks[4 * q + 3]);
-            store16(out + 64 * j + 16 * q, c[q], ALIGNED);
+            const uint4 c = make_uint4(d[q].x ^ ks[4 * q], d[q].y ^ ks[4 * q + 1],
+                                       d[q].z ^ ks[4 * q + 2], d[q].w ^ ks[4 * q + 3]);
+            store16(out + 64 * j + 16 * q, c, ALIGNED);
+            m[q] = OPEN ? d[q] : c;
         }
+        // payload of block j+1 in flight (the last iteration re-reads block j: in bounds)
+        const uint32_t jn = j + 1 < nfull ? j + 1 : j;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) d[q] = load16(in + 64 * jn + 16 * q, ALIGNED);
         chacha_block(k, j + 2, nv.x, nv.y, nv.z, ks);
 #pragma unroll
-        for (int q = 0; q < 4; ++q) poly_block(p, OPEN ? d[q] : c[q]);
-#pragma unroll
-        for (int q = 0; q < 4; ++q) d[q] = nx[q];
+        for (int q = 0; q < 4; ++q) poly_block(p, m[q]);
     }
 }
 

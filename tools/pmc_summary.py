@@ -7,12 +7,9 @@ from collections import defaultdict
 
 
 def short(name):
-    for k in ("gcm_kernel<10, false>", "gcm_kernel<10, true>", "gcm_kernel<14, false>",
-              "gcm_kernel<14, true>", "chacha_kernel<false, false>", "chacha_kernel<true, false>",
-              "chacha_kernel<false, true>", "chacha_kernel<true, true>"):
-        if k in name:
-            return k
-    return None
+    import re
+    m = re.search(r"(gcm_kernel<[^>]*>|chacha_kernel<[^>]*>|k_copy_\w+)", name)
+    return m.group(1) if m else None
 
 
 def main(d):
