@@ -139,14 +139,13 @@ __device__ __forceinline__ uint4 poly_finish(const Poly& p) {
 // ALIGNED records use 16-byte vector loads and stores with no branches.
 template <bool OPEN, bool ALIGNED>
 __device__ __forceinline__ void full_blocks(const uint32_t (&k)[8], uint4 nv, const uint8_t* in,
-                                            uint8_t* out, uint32_t nfull, Poly& p,
+                                            uint8_t* out, uint32_t j0, uint32_t nfull, Poly& p,
                                             uint32_t (&ks)[16]) {
-    chacha_block(k, 1, nv.x, nv.y, nv.z, ks);
-    if (nfull == 0) return;
+    if (j0 >= nfull) return;
     uint4 d[4];
 #pragma unroll
-    for (int q = 0; q < 4; ++q) d[q] = load16(in + 16 * q, ALIGNED);
-    for (uint32_t j = 0; j < nfull; ++j) {
+    for (int q = 0; q < 4; ++q) d[q] = load16(in + 64 * j0 + 16 * q, ALIGNED);
+    for (uint32_t j = j0; j < nfull; ++j) {
         // m = the Poly1305 input of block j (ciphertext: c for seal, d for open)
         uint4 m[4];
 #pragma unroll
@@ -166,11 +165,99 @@ __device__ __forceinline__ void full_blocks(const uint32_t (&k)[8], uint4 nv, co
     }
 }
 
+__device__ __forceinline__ uint32_t wave_min(uint32_t v) {
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t w = (uint32_t)__shfl_xor((int)v, o);
+        v = w < v ? w : v;
+    }
+    return v;
+}
+
+// Per-wave LDS: a 64-record x 64-byte tile (row r = the record of lane r, its
+// four 16-byte chunks XOR-swizzled by (r >> 2) & 3 so that both the row-wise
+// and the coalesced accesses are bank-conflict-free) and the records' in/out
+// base pointers.
+struct WaveTile {
+    uint4 row[64][4];
+    uint4 ptr[64];  // {in lo, in hi, out lo, out hi}
+};
+constexpr int kWavesPerGroup = kChachaThreads / 64;
+
+__device__ __forceinline__ uint32_t swz(uint32_t r, uint32_t c) { return c ^ ((r >> 2) & 3); }
+
+// Blocks [0, jmin) of all 64 records of a wave (every record has >= jmin full
+// blocks and 16-byte aligned buffers).  HBM traffic is coalesced through the
+// tile: for load/store instruction q, lane L moves chunk L%4 of record
+// 16q + L/4, i.e. 16 records x 64 contiguous bytes per instruction, instead of
+// 64 scattered 16-byte pieces.  The keystream/Poly1305 pipeline is the same as
+// full_blocks().
+template <bool OPEN>
+__device__ __forceinline__ void tiled_blocks(WaveTile& t, uint32_t lane, uint32_t nvalid,
+                                             const uint32_t (&k)[8], uint4 nv, uint32_t jmin,
+                                             Poly& p, uint32_t (&ks)[16]) {
+    const uint32_t cq = lane & 3;
+    uint4 R[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const uint32_t r = 16 * q + (lane >> 2);
+        const uint4 pr = t.ptr[r];
+        const uint8_t* src = reinterpret_cast<const uint8_t*>(((uint64_t)pr.y << 32) | pr.x);
+        R[q] = r < nvalid ? *reinterpret_cast<const uint4*>(src + 16 * cq) : make_uint4(0, 0, 0, 0);
+    }
+    for (uint32_t j = 0; j < jmin; ++j) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const uint32_t r = 16 * q + (lane >> 2);
+            t.row[r][swz(r, cq)] = R[q];
+        }
+        __builtin_amdgcn_wave_barrier();
+        const uint32_t jn = j + 1 < jmin ? j + 1 : j;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const uint32_t r = 16 * q + (lane >> 2);
+            const uint4 pr = t.ptr[r];
+            const uint8_t* src = reinterpret_cast<const uint8_t*>(((uint64_t)pr.y << 32) | pr.x);
+            if (r < nvalid) R[q] = *reinterpret_cast<const uint4*>(src + 64 * jn + 16 * cq);
+        }
+        uint4 m[4];
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            const uint4 d = t.row[lane][swz(lane, c)];
+            const uint4 ct = make_uint4(d.x ^ ks[4 * c], d.y ^ ks[4 * c + 1], d.z ^ ks[4 * c + 2],
+                                        d.w ^ ks[4 * c + 3]);
+            t.row[lane][swz(lane, c)] = ct;
+            m[c] = OPEN ? d : ct;
+        }
+        __builtin_amdgcn_wave_barrier();
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const uint32_t r = 16 * q + (lane >> 2);
+            const uint4 v = t.row[r][swz(r, cq)];
+            const uint4 pr = t.ptr[r];
+            uint8_t* dst = reinterpret_cast<uint8_t*>(((uint64_t)pr.w << 32) | pr.z);
+            if (r < nvalid) *reinterpret_cast<uint4*>(dst + 64 * j + 16 * cq) = v;
+        }
+        __builtin_amdgcn_wave_barrier();
+        chacha_block(k, j + 2, nv.x, nv.y, nv.z, ks);
+#pragma unroll
+        for (int c = 0; c < 4; ++c) poly_block(p, m[c]);
+    }
+}
+
 template <bool OPEN, bool MULTIKEY>
 __global__ __launch_bounds__(kChachaThreads) void chacha_kernel(
     const ChachaKeyDev* __restrict__ keys, tg_batch b) {
-    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= b.n) return;
+    __shared__ WaveTile tiles[kWavesPerGroup];
+    const uint64_t i_raw = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t lane = threadIdx.x & 63;
+    const uint64_t wave_base = i_raw - lane;
+    if (wave_base >= b.n) return;  // whole wave idle (uniform)
+    // Lanes past the end of the batch stay alive to serve the wave's
+    // coalesced transfers, but work on a clamped record and never store.
+    const bool valid = i_raw < b.n;
+    const uint64_t i = valid ? i_raw : b.n - 1;
+    const uint32_t nvalid = b.n - wave_base < 64 ? (uint32_t)(b.n - wave_base) : 64u;
     uint32_t k[8];
     const ChachaKeyDev* kp = keys + (MULTIKEY ? b.key_idx[i] : 0);
 #pragma unroll
@@ -198,11 +285,26 @@ __global__ __launch_bounds__(kChachaThreads) void chacha_kernel(
 
     const uint32_t nfull = len >> 6;
     uint32_t ks[16];
-    if (aligned) {
-        full_blocks<OPEN, true>(k, nv, in, out, nfull, p, ks);
-    } else {
-        full_blocks<OPEN, false>(k, nv, in, out, nfull, p, ks);
+    chacha_block(k, 1, nv.x, nv.y, nv.z, ks);
+    // Coalesced tile path for the blocks every record of the wave has.
+    const uint32_t jmin = __all(!valid || aligned) ? wave_min(valid ? nfull : 0xffffffffu) : 0;
+    uint32_t j0 = 0;
+    if (jmin > 0) {
+        WaveTile& t = tiles[threadIdx.x >> 6];
+        t.ptr[lane] = make_uint4((uint32_t)(uintptr_t)in, (uint32_t)((uintptr_t)in >> 32),
+                                 (uint32_t)(uintptr_t)out, (uint32_t)((uintptr_t)out >> 32));
+        __builtin_amdgcn_wave_barrier();
+        tiled_blocks<OPEN>(t, lane, nvalid, k, nv, jmin, p, ks);
+        j0 = jmin;
     }
+    if (valid) {
+        if (aligned) {
+            full_blocks<OPEN, true>(k, nv, in, out, j0, nfull, p, ks);
+        } else {
+            full_blocks<OPEN, false>(k, nv, in, out, j0, nfull, p, ks);
+        }
+    }
+    if (!valid) return;
     const uint32_t rem = len - 64 * nfull;
     if (rem) {  // ks already holds keystream block nfull + 1
 #pragma unroll
