@@ -93,6 +93,8 @@ def main():
     ap.add_argument("--cpu-records", type=int, default=6)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--e2e", action="store_true", help="also time the host<->device path")
+    ap.add_argument("--record-align", type=int, default=128,
+                    help="byte alignment of each sealed record (ct||tag) in the packed batch")
     args = ap.parse_args()
 
     import torch
@@ -108,10 +110,13 @@ def main():
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
 
     n, L = args.records, args.len
+    # sealed records are ct||tag (the wire form), packed at a stride rounded up
+    # to --record-align bytes so every record starts on an HBM line boundary
+    SL = (L + TAG_LEN + args.record_align - 1) // args.record_align * args.record_align
     dev = "cuda"
     g = torch.Generator(device=dev).manual_seed(0x7715 + rank)
     inp = torch.randint(0, 256, (n * L,), dtype=torch.uint8, device=dev, generator=g)
-    sealed = torch.empty(n * (L + TAG_LEN), dtype=torch.uint8, device=dev)
+    sealed = torch.empty(n * SL, dtype=torch.uint8, device=dev)
     back = torch.empty(n * L, dtype=torch.uint8, device=dev)
     status = torch.zeros(n, dtype=torch.uint8, device=dev)
     nonces = torch.empty(NONCE_LEN * n, dtype=torch.uint8, device=dev)
@@ -126,9 +131,9 @@ def main():
     # this rank's records are seq [rank*n, (rank+1)*n) of one connection
     tlsgpu.make_nonces(iv, rank * n, n, nonces)
     seal_b = tlsgpu.make_batch(n, inp, sealed, nonces, aad=aad, fixed_len=L, in_stride=L,
-                               out_stride=L + TAG_LEN, fixed_aad_len=AAD_LEN)
+                               out_stride=SL, fixed_aad_len=AAD_LEN)
     open_b = tlsgpu.make_batch(n, sealed, back, nonces, aad=aad, fixed_len=L,
-                               in_stride=L + TAG_LEN, out_stride=L, fixed_aad_len=AAD_LEN,
+                               in_stride=SL, out_stride=L, fixed_aad_len=AAD_LEN,
                                status=status)
     stream = torch.cuda.current_stream()
     kinds = [(a, op) for a in ciphers for op in ("seal", "open")]
@@ -205,6 +210,7 @@ def main():
             "config": {"workload": "BASELINE configs[1]+[2]: 2^20 x 16 KiB TLS 1.3 records per GPU, "
                                    "single key, AES-128-GCM and ChaCha20-Poly1305, seal+open",
                        "records_per_gpu": n, "record_len": L, "aad_len": AAD_LEN,
+                       "sealed_stride": SL,
                        "parallelism": "records sharded by seq range, %d rank(s)" % world},
             "per_kernel": per_kernel,
             "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(dom_achieved, 1),
