@@ -144,15 +144,18 @@ def test_batch_ragged_vs_oracle(torch, tg, oracle_mod, alg, klen, align):
                    tamper=(3, 17, 100))
 
 
-def test_chacha_key_table_vs_oracle(torch, tg, oracle_mod):
+@pytest.mark.parametrize("alg,klen", [("chacha", 32), ("aesgcm", 16), ("aesgcm", 32)])
+@pytest.mark.parametrize("align", [16, 1])
+def test_key_table_vs_oracle(torch, tg, oracle_mod, alg, klen, align):
+    """Many sessions in one batch (BASELINE config 4 shape): key_idx per record."""
     from batchpack import HostBatch
-    rng = np.random.default_rng(5)
-    lens = list(rng.integers(0, 4097, 700))
-    hb = HostBatch(lens, payload_seed=9, aad_mode="tls12", key_count=37)
-    keys = [rng.bytes(32) for _ in range(37)]
-    table = tg.KeyTable("chacha20-poly1305", keys)
-    karr = np.frombuffer(b"".join(keys), np.uint8).reshape(37, 32)
-    _run_seal_open(torch, tg, oracle_mod, hb, "chacha", karr, table, tamper=(1, 500))
+    rng = np.random.default_rng(5 + klen + align)
+    lens = list(rng.integers(0, 4097, 700)) + [0, 1, 15, 16, 17, 16384, 16400]
+    hb = HostBatch(lens, payload_seed=9, align=align, aad_mode="tls12", key_count=37)
+    keys = [rng.bytes(klen) for _ in range(37)]
+    table = tg.KeyTable("chacha20-poly1305" if alg == "chacha" else "aesgcm", keys)
+    karr = np.frombuffer(b"".join(keys), np.uint8).reshape(37, klen)
+    _run_seal_open(torch, tg, oracle_mod, hb, alg, karr, table, tamper=(1, 500))
 
 
 def test_record_batch_fixtures(torch, tg):

@@ -79,6 +79,13 @@ typedef const __attribute__((address_space(3))) uint32_t* lds_u32_ptr;
 typedef const __attribute__((address_space(3))) uint4* lds_u128_ptr;
 __device__ __forceinline__ uint32_t lds_u32(uint32_t addr) { return *(lds_u32_ptr)(uintptr_t)addr; }
 __device__ __forceinline__ uint4 lds_u128(uint32_t addr) { return *(lds_u128_ptr)(uintptr_t)addr; }
+__device__ __forceinline__ uint4 lds_u128_v(uint32_t addr) {
+    const volatile __attribute__((address_space(3))) uint4* p =
+        (const volatile __attribute__((address_space(3))) uint4*)(uintptr_t)addr;
+    uint4 v;
+    v.x = p->x; v.y = p->y; v.z = p->z; v.w = p->w;
+    return v;
+}
 __device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
     return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
 }
@@ -88,6 +95,7 @@ __device__ __forceinline__ uint32_t and_or(uint32_t a, uint32_t b, uint32_t c) {
 #else
 __device__ __forceinline__ uint32_t lds_u32(uint32_t) { return 0; }
 __device__ __forceinline__ uint4 lds_u128(uint32_t) { return uint4(); }
+__device__ __forceinline__ uint4 lds_u128_v(uint32_t) { return uint4(); }
 __device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) { return a ^ b ^ c; }
 __device__ __forceinline__ uint32_t and_or(uint32_t a, uint32_t b, uint32_t c) { return (a & b) | c; }
 #endif
@@ -123,6 +131,20 @@ __device__ __forceinline__ uint32_t col_last(uint32_t sa, uint32_t sb, uint32_t 
     return xor3(lo, hi, rk);
 }
 
+// Round-key providers: get(r) = the four words of round key r.
+template <int NR>
+struct RkRegs {  // single key per launch: wave-uniform, lives in SGPRs
+    uint32_t w[4 * (NR + 1)];
+    __device__ __forceinline__ uint4 get(int r) const {
+        return make_uint4(w[4 * r], w[4 * r + 1], w[4 * r + 2], w[4 * r + 3]);
+    }
+};
+struct RkLds {  // key table: this lane's schedule staged in an LDS row
+    uint32_t base;
+    // volatile: re-read per round instead of being hoisted into 60 VGPRs
+    __device__ __forceinline__ uint4 get(int r) const { return lds_u128_v(base + 16 * r); }
+};
+
 // Per-record round-1 constants for counter mode: after AddRoundKey the state
 // words s0..s2 (nonce ^ rk0) are the same for every block of the record, so
 // each round-1 column is a constant K_c XOR the one term that reads s3.
@@ -130,10 +152,11 @@ struct CtrCache {
     uint32_t k0, k1, k2, k3;
 };
 
-template <int NR>
-__device__ __forceinline__ CtrCache ctr_cache(uint32_t lane4, const uint32_t (&rk)[4 * (NR + 1)],
-                                              uint4 nv) {
-    const uint32_t s0 = nv.x ^ rk[0], s1 = nv.y ^ rk[1], s2 = nv.z ^ rk[2];
+template <int NR, class RK>
+__device__ __forceinline__ CtrCache ctr_cache(uint32_t lane4, const RK& rkp, uint4 nv) {
+    const uint4 k0 = rkp.get(0), k1 = rkp.get(1);
+    const uint32_t s0 = nv.x ^ k0.x, s1 = nv.y ^ k0.y, s2 = nv.z ^ k0.z;
+    const uint32_t rk[8] = {k0.x, k0.y, k0.z, k0.w, k1.x, k1.y, k1.z, k1.w};
     CtrCache c;
     // column 0: a=s0.b0 b=s1.b1 c=s2.b2 d=s3.b3(varies)
     c.k0 = T0<0>(s0, lane4) ^ T2<2>(s2, lane4) ^ rotl32(T0<1>(s1, lane4), 8) ^ rk[4];
@@ -147,10 +170,10 @@ __device__ __forceinline__ CtrCache ctr_cache(uint32_t lane4, const uint32_t (&r
 }
 
 // E_K(nonce || be32(ctr)) using the round-1 cache.
-template <int NR>
-__device__ __forceinline__ uint4 aes_ctr(uint32_t lane4, const uint32_t (&rk)[4 * (NR + 1)],
-                                         const CtrCache& cc, uint32_t ctr) {
-    uint32_t s3 = bswap32(ctr) ^ rk[3];
+template <int NR, class RK>
+__device__ __forceinline__ uint4 aes_ctr(uint32_t lane4, const RK& rkp, const CtrCache& cc,
+                                         uint32_t ctr) {
+    uint32_t s3 = bswap32(ctr) ^ rkp.get(0).w;
     uint32_t s0 = cc.k0 ^ rotl32(T2<3>(s3, lane4), 8);
     uint32_t s1 = cc.k1 ^ T2<2>(s3, lane4);
     uint32_t s2 = cc.k2 ^ rotl32(T0<1>(s3, lane4), 8);
@@ -159,16 +182,16 @@ __device__ __forceinline__ uint4 aes_ctr(uint32_t lane4, const uint32_t (&rk)[4 
     s3 = t3;
 #pragma unroll
     for (int r = 2; r < NR; ++r) {
-        t0 = col(s0, s1, s2, s3, rk[4 * r], lane4);
-        t1 = col(s1, s2, s3, s0, rk[4 * r + 1], lane4);
-        t2 = col(s2, s3, s0, s1, rk[4 * r + 2], lane4);
-        t3 = col(s3, s0, s1, s2, rk[4 * r + 3], lane4);
+        const uint4 k = rkp.get(r);
+        t0 = col(s0, s1, s2, s3, k.x, lane4);
+        t1 = col(s1, s2, s3, s0, k.y, lane4);
+        t2 = col(s2, s3, s0, s1, k.z, lane4);
+        t3 = col(s3, s0, s1, s2, k.w, lane4);
         s0 = t0; s1 = t1; s2 = t2; s3 = t3;
     }
-    return make_uint4(col_last(s0, s1, s2, s3, rk[4 * NR], lane4),
-                      col_last(s1, s2, s3, s0, rk[4 * NR + 1], lane4),
-                      col_last(s2, s3, s0, s1, rk[4 * NR + 2], lane4),
-                      col_last(s3, s0, s1, s2, rk[4 * NR + 3], lane4));
+    const uint4 k = rkp.get(NR);
+    return make_uint4(col_last(s0, s1, s2, s3, k.x, lane4), col_last(s1, s2, s3, s0, k.y, lane4),
+                      col_last(s2, s3, s0, s1, k.z, lane4), col_last(s3, s0, s1, s2, k.w, lane4));
 }
 
 // y * H with the sixteen 8-bit tables: X * H = XOR_j M_j[byte j of X]; byte j
@@ -196,12 +219,93 @@ __device__ __forceinline__ uint4 gmul(uint4 y) {
     return xor4(z, e[15]);
 }
 
+struct GhashTables {  // single key: the 8-bit tables staged in LDS; y in block byte layout
+    __device__ __forceinline__ uint4 update(uint4 y, uint4 blk) const { return gmul(xor4(y, blk)); }
+    __device__ __forceinline__ uint4 finish(uint4 y) const { return y; }
+};
+
+// ---- table-free GHASH for key tables -----------------------------------
+// A key table cannot stage 64 KiB of GHASH tables per session, so each lane
+// multiplies by its own H with a carry-less multiply built from integer
+// multiplies (bits spaced four apart cannot carry into each other: a product
+// of two such words, masked to one residue class mod 4, is the carry-less
+// product on that class).  Elements are kept in normal polynomial order
+// (coefficient of x^i at bit i): a GCM block's bytes keep their positions and
+// each byte is bit-reversed (aesgcm.py:8-14).
+__device__ __forceinline__ uint32_t to_norm(uint32_t w) {
+    return bswap32(__builtin_bitreverse32(w));
+}
+
+__device__ __forceinline__ uint64_t mul32(uint32_t a, uint32_t b) { return (uint64_t)a * b; }
+
+__device__ __forceinline__ uint64_t clmul32(uint32_t x, uint32_t y) {
+    const uint32_t x0 = x & 0x11111111u, x1 = x & 0x22222222u, x2 = x & 0x44444444u,
+                   x3 = x & 0x88888888u;
+    const uint32_t y0 = y & 0x11111111u, y1 = y & 0x22222222u, y2 = y & 0x44444444u,
+                   y3 = y & 0x88888888u;
+    const uint64_t z0 = mul32(x0, y0) ^ mul32(x1, y3) ^ mul32(x2, y2) ^ mul32(x3, y1);
+    const uint64_t z1 = mul32(x0, y1) ^ mul32(x1, y0) ^ mul32(x2, y3) ^ mul32(x3, y2);
+    const uint64_t z2 = mul32(x0, y2) ^ mul32(x1, y1) ^ mul32(x2, y0) ^ mul32(x3, y3);
+    const uint64_t z3 = mul32(x0, y3) ^ mul32(x1, y2) ^ mul32(x2, y1) ^ mul32(x3, y0);
+    return (z0 & 0x1111111111111111ull) | (z1 & 0x2222222222222222ull) |
+           (z2 & 0x4444444444444444ull) | (z3 & 0x8888888888888888ull);
+}
+
+// 64 x 64 -> 128 by one Karatsuba step over 32-bit halves; result words w0..w3.
+// sched_barrier between the 32-bit products keeps the scheduler from running
+// all nine at once (each holds 16 64-bit partial products).
+__device__ __forceinline__ uint4 clmul64(uint32_t a0, uint32_t a1, uint32_t b0, uint32_t b1) {
+    const uint64_t lo = clmul32(a0, b0);
+    __builtin_amdgcn_sched_barrier(0);
+    const uint64_t hi = clmul32(a1, b1);
+    __builtin_amdgcn_sched_barrier(0);
+    const uint64_t mid = clmul32(a0 ^ a1, b0 ^ b1) ^ lo ^ hi;
+    __builtin_amdgcn_sched_barrier(0);
+    return make_uint4((uint32_t)lo, (uint32_t)(lo >> 32) ^ (uint32_t)mid,
+                      (uint32_t)(mid >> 32) ^ (uint32_t)hi, (uint32_t)(hi >> 32));
+}
+
+// a * b mod x^128 + x^7 + x^2 + x + 1, normal order, 32-bit limbs (x^0 in .x).
+__device__ __forceinline__ uint4 gf128_mul(uint4 a, uint4 b) {
+    const uint4 L = clmul64(a.x, a.y, b.x, b.y);
+    const uint4 Hh = clmul64(a.z, a.w, b.z, b.w);
+    const uint4 M = clmul64(a.x ^ a.z, a.y ^ a.w, b.x ^ b.z, b.y ^ b.w);
+    const uint32_t m0 = xor3(M.x, L.x, Hh.x), m1 = xor3(M.y, L.y, Hh.y);
+    const uint32_t m2 = xor3(M.z, L.z, Hh.z), m3 = xor3(M.w, L.w, Hh.w);
+    // 256-bit product p0..p7
+    const uint32_t p0 = L.x, p1 = L.y, p2 = L.z ^ m0, p3 = L.w ^ m1;
+    const uint32_t t0 = Hh.x ^ m2, t1 = Hh.y ^ m3, t2 = Hh.z, t3 = Hh.w;
+    // fold T = p4..p7 (x^128 == x^7 + x^2 + x + 1): r ^= T ^ T<<1 ^ T<<2 ^ T<<7
+    const uint32_t v = (t3 >> 31) ^ (t3 >> 30) ^ (t3 >> 25);  // bits pushed past x^127
+    uint32_t r0 = xor3(p0, t0, t0 << 1) ^ xor3(t0 << 2, t0 << 7, v);
+    r0 ^= xor3(v << 1, v << 2, v << 7);
+    const uint32_t r1 = xor3(p1, t1, t1 << 1) ^ xor3(t1 << 2, t1 << 7, (t0 >> 31)) ^
+                        ((t0 >> 30) ^ (t0 >> 25));
+    const uint32_t r2 = xor3(p2, t2, t2 << 1) ^ xor3(t2 << 2, t2 << 7, (t1 >> 31)) ^
+                        ((t1 >> 30) ^ (t1 >> 25));
+    const uint32_t r3 = xor3(p3, t3, t3 << 1) ^ xor3(t3 << 2, t3 << 7, (t2 >> 31)) ^
+                        ((t2 >> 30) ^ (t2 >> 25));
+    return make_uint4(r0, r1, r2, r3);
+}
+
+struct GhashClmul {  // y kept in normal order; hn = H in normal order
+    uint4 hn;
+    __device__ __forceinline__ uint4 update(uint4 y, uint4 blk) const {
+        const uint4 x = make_uint4(y.x ^ to_norm(blk.x), y.y ^ to_norm(blk.y),
+                                   y.z ^ to_norm(blk.z), y.w ^ to_norm(blk.w));
+        return gf128_mul(x, hn);
+    }
+    __device__ __forceinline__ uint4 finish(uint4 y) const {
+        return make_uint4(to_norm(y.x), to_norm(y.y), to_norm(y.z), to_norm(y.w));
+    }
+};
+
 // Full 16-byte blocks [0, G*ngroups) in groups of G.  The keystream of group
 // g+1 and the payload of group g+1 are produced while group g is XORed and
 // hashed, so the GHASH chain of seal (which needs the ciphertext) overlaps the
 // next group's AES rounds.
-template <int NR, bool OPEN, bool ALIGNED, int G>
-__device__ __forceinline__ uint4 ctr_groups(uint32_t lane4, const uint32_t (&rk)[4 * (NR + 1)],
+template <int NR, bool OPEN, bool ALIGNED, int G, class RK, class GH>
+__device__ __forceinline__ uint4 ctr_groups(uint32_t lane4, const RK& rk, const GH& gh,
                                             const CtrCache& cc, const uint8_t* in, uint8_t* out,
                                             uint32_t ngroups, uint4 y) {
     if (ngroups == 0) return y;
@@ -223,35 +327,17 @@ __device__ __forceinline__ uint4 ctr_groups(uint32_t lane4, const uint32_t (&rk)
 #pragma unroll
         for (int q = 0; q < G; ++q) ks[q] = aes_ctr<NR>(lane4, rk, cc, 2u + G * (g + 1) + q);
 #pragma unroll
-        for (int q = 0; q < G; ++q) y = gmul(xor4(y, OPEN ? d[q] : c[q]));
+        for (int q = 0; q < G; ++q) y = gh.update(y, OPEN ? d[q] : c[q]);
 #pragma unroll
         for (int q = 0; q < G; ++q) d[q] = nx[q];
     }
     return y;
 }
 
-template <int NR, bool OPEN, int G, int THREADS>
-__global__ __launch_bounds__(THREADS) void gcm_kernel(const GcmKeyDev* __restrict__ key,
-                                                      tg_batch b) {
-    uint4* lds = g_lds;
-    // stage the GHASH tables and the Te0/Te2 copies
-    for (int e = threadIdx.x; e < kGhashEntries; e += blockDim.x) lds[e] = key->ghash[e];
-    {
-        uint32_t* te = reinterpret_cast<uint32_t*>(lds) + kTeBase / 4;
-        for (int e = threadIdx.x; e < 256 * 64; e += blockDim.x) {
-            const uint32_t v = c_te.te0[e >> 6];
-            te[e] = (e & 32) ? rotl32(v, 16) : v;
-        }
-    }
-    uint32_t rk[4 * (NR + 1)];
-#pragma unroll
-    for (int k = 0; k < 4 * (NR + 1); ++k) rk[k] = key->rk[k];
-    __syncthreads();
-
-    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= b.n) return;
-    const uint32_t lane4 = ((threadIdx.x & 31u) << 2) | kTeBase;
-
+// One record: AESGCM.seal / AESGCM.open (aesgcm.py:101-154) for lane i.
+template <int NR, bool OPEN, int G, class RK, class GH>
+__device__ __forceinline__ void gcm_record(const tg_batch& b, uint64_t i, uint32_t lane4,
+                                           const RK& rk, const GH& gh) {
     const uint8_t* in = rec_in(b, i);
     uint8_t* out = rec_out(b, i);
     const uint32_t len = rec_len(b, i);
@@ -268,35 +354,35 @@ __global__ __launch_bounds__(THREADS) void gcm_kernel(const GcmKeyDev* __restric
     uint4 y = make_uint4(0, 0, 0, 0);
     for (uint32_t off = 0; off < alen; off += 16) {
         uint32_t m = alen - off < 16 ? alen - off : 16;
-        y = gmul(xor4(y, load_partial(ad + off, m)));
+        y = gh.update(y, load_partial(ad + off, m));
     }
 
     // CTR from nonce || be32(2) (aesgcm.py:118-120), GHASH over the ciphertext
     const uint32_t nfull = len >> 4;
     const uint32_t tail = len & 15;
     const uint32_t ngroups = nfull / G;
-    y = aligned ? ctr_groups<NR, OPEN, true, G>(lane4, rk, cc, in, out, ngroups, y)
-                : ctr_groups<NR, OPEN, false, G>(lane4, rk, cc, in, out, ngroups, y);
+    y = aligned ? ctr_groups<NR, OPEN, true, G>(lane4, rk, gh, cc, in, out, ngroups, y)
+                : ctr_groups<NR, OPEN, false, G>(lane4, rk, gh, cc, in, out, ngroups, y);
     for (uint32_t j = G * ngroups; j < nfull; ++j) {
         const uint4 ks = aes_ctr<NR>(lane4, rk, cc, 2u + j);
         const uint4 d = load16(in + 16 * j, aligned);
         const uint4 c = xor4(d, ks);
         store16(out + 16 * j, c, aligned);
-        y = gmul(xor4(y, OPEN ? d : c));
+        y = gh.update(y, OPEN ? d : c);
     }
     if (tail) {
         const uint4 ks = aes_ctr<NR>(lane4, rk, cc, 2u + nfull);
         const uint4 d = load_partial(in + 16 * nfull, tail);
         const uint4 c = mask_tail(xor4(d, ks), tail);
         store_partial(out + 16 * nfull, c, tail);
-        y = gmul(xor4(y, OPEN ? d : c));
+        y = gh.update(y, OPEN ? d : c);
     }
 
     // length block: be64(8*alen) || be64(8*len) (aesgcm.py:64)
     const uint64_t abits = (uint64_t)alen << 3, cbits = (uint64_t)len << 3;
-    y = gmul(xor4(y, make_uint4(bswap32((uint32_t)(abits >> 32)), bswap32((uint32_t)abits),
-                                bswap32((uint32_t)(cbits >> 32)), bswap32((uint32_t)cbits))));
-    const uint4 tag = xor4(y, mask);
+    y = gh.update(y, make_uint4(bswap32((uint32_t)(abits >> 32)), bswap32((uint32_t)abits),
+                                bswap32((uint32_t)(cbits >> 32)), bswap32((uint32_t)cbits)));
+    const uint4 tag = xor4(gh.finish(y), mask);
     if (!OPEN) {
         store16(out + len, tag, aligned && tail == 0);
         return;
@@ -310,6 +396,63 @@ __global__ __launch_bounds__(THREADS) void gcm_kernel(const GcmKeyDev* __restric
         for (uint32_t k = 0; k < nfull; ++k) store16(out + 16 * k, z, aligned);
         if (tail) store_partial(out + 16 * nfull, z, tail);
     }
+}
+
+
+template <int NR, bool OPEN, int G, int THREADS>
+__global__ __launch_bounds__(THREADS) void gcm_kernel(const GcmKeyDev* __restrict__ key,
+                                                      tg_batch b) {
+    uint4* lds = g_lds;
+    // stage the GHASH tables and the Te0/Te2 copies
+    for (int e = threadIdx.x; e < kGhashEntries; e += blockDim.x) lds[e] = key->ghash[e];
+    {
+        uint32_t* te = reinterpret_cast<uint32_t*>(lds) + kTeBase / 4;
+        for (int e = threadIdx.x; e < 256 * 64; e += blockDim.x) {
+            const uint32_t v = c_te.te0[e >> 6];
+            te[e] = (e & 32) ? rotl32(v, 16) : v;
+        }
+    }
+    RkRegs<NR> rk;
+#pragma unroll
+    for (int k = 0; k < 4 * (NR + 1); ++k) rk.w[k] = key->rk[k];
+    const GhashTables gh;
+    __syncthreads();
+
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= b.n) return;
+    const uint32_t lane4 = ((threadIdx.x & 31u) << 2) | kTeBase;
+    gcm_record<NR, OPEN, G>(b, i, lane4, rk, gh);
+}
+
+// Key-table kernel (many sessions per batch, BASELINE config 4): lane i uses
+// key key_idx[i]; its round keys are staged into a private LDS row (272-byte
+// stride: conflict-free ds_read_b128) and GHASH is the table-free multiply.
+constexpr int kMkThreads = 256;
+constexpr uint32_t kMkRowBytes = 272;
+constexpr size_t kMkLds = 65536 + kMkThreads * kMkRowBytes;
+
+template <int NR, bool OPEN, int G>
+__global__ __launch_bounds__(kMkThreads, 4) void gcm_table_kernel(const GcmTableKey* __restrict__ keys,
+                                                              tg_batch b) {
+    uint4* lds = g_lds;
+    {
+        uint32_t* te = reinterpret_cast<uint32_t*>(lds);  // Te0/Te2 copies at LDS 0
+        for (int e = threadIdx.x; e < 256 * 64; e += blockDim.x) {
+            const uint32_t v = c_te.te0[e >> 6];
+            te[e] = (e & 32) ? rotl32(v, 16) : v;
+        }
+    }
+    __syncthreads();
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= b.n) return;
+    const GcmTableKey* kp = keys + b.key_idx[i];
+    const RkLds rk{65536u + threadIdx.x * kMkRowBytes};
+    uint4* row = lds + rk.base / 16;
+#pragma unroll
+    for (int r = 0; r <= NR; ++r) row[r] = reinterpret_cast<const uint4*>(kp->rk)[r];
+    const GhashClmul gh{*reinterpret_cast<const uint4*>(kp->hn)};
+    const uint32_t lane4 = (threadIdx.x & 31u) << 2;
+    gcm_record<NR, OPEN, G>(b, i, lane4, rk, gh);
 }
 
 template <int NR, bool OPEN, int G, int THREADS>
@@ -349,8 +492,33 @@ int launch(const GcmKeyDev* key, const tg_batch& b, hipStream_t s) {
     }
 }
 
+template <int NR, bool OPEN>
+int launch_table(const GcmTableKey* keys, const tg_batch& b, hipStream_t s) {
+    static bool attr_set = false;
+    if (!attr_set) {
+        if (hipFuncSetAttribute((const void*)gcm_table_kernel<NR, OPEN, 1>,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)kMkLds) !=
+            hipSuccess)
+            return TG_EHIP;
+        attr_set = true;
+    }
+    const uint64_t blocks = (b.n + kMkThreads - 1) / kMkThreads;
+    hipLaunchKernelGGL((gcm_table_kernel<NR, OPEN, 1>), dim3((unsigned)blocks), dim3(kMkThreads),
+                       kMkLds, s, keys, b);  // G = 1: one block in flight per lane
+    return hipGetLastError() == hipSuccess ? TG_OK : TG_EHIP;
+}
+
 }  // namespace
 }  // namespace tg
+
+int tg_launch_gcm_table(const tg::GcmTableKey* keys, int rounds, const tg_batch& b, bool open,
+                        hipStream_t s) {
+    if (rounds == 10)
+        return open ? tg::launch_table<10, true>(keys, b, s) : tg::launch_table<10, false>(keys, b, s);
+    if (rounds == 14)
+        return open ? tg::launch_table<14, true>(keys, b, s) : tg::launch_table<14, false>(keys, b, s);
+    return TG_EINVAL;
+}
 
 int tg_launch_gcm(const tg::GcmKeyDev* key, int rounds, const tg_batch& b, bool open,
                   hipStream_t s) {

@@ -193,6 +193,9 @@ int ensure_stage(tg_key* k, size_t bytes) {
 }
 
 int launch(tg_key* k, const tg_batch& b, bool open, hipStream_t s) {
+    if (k->alg == TG_AES_GCM && k->nkeys > 1)
+        return tg_launch_gcm_table(static_cast<const tg::GcmTableKey*>(k->dev_key), k->rounds, b,
+                                   open, s);
     if (k->alg == TG_AES_GCM)
         return tg_launch_gcm(static_cast<const tg::GcmKeyDev*>(k->dev_key), k->rounds, b, open, s);
     return tg_launch_chacha(static_cast<const tg::ChachaKeyDev*>(k->dev_key), b, open, s);
@@ -204,6 +207,7 @@ size_t align16(size_t v) { return (v + 15) & ~(size_t)15; }
 int single(tg_key* k, const uint8_t* nonce, size_t noncelen, const uint8_t* aad, size_t aadlen,
            const uint8_t* in, size_t inlen, uint8_t* out, bool open) {
     if (!k) return fail(TG_EINVAL, "null key");
+    if (k->nkeys != 1) return fail(TG_EINVAL, "per-record calls need a single-key handle");
     if (noncelen != 12) return fail(TG_ENONCE, "Bad nonce length");
     if ((aadlen && !aad) || (inlen && !in)) return fail(TG_EINVAL, "null buffer");
     if (open && inlen < 16) {   // aesgcm.py:135-136, chacha20_poly1305.py:76-77
@@ -251,8 +255,7 @@ int batch(tg_key* k, const tg_batch* b, void* stream, bool open) {
     if (!b->in || !b->out || !b->nonce) return fail(TG_EINVAL, "null device buffer");
     if (!b->aad && (b->aad_len || b->fixed_aad_len)) return fail(TG_EINVAL, "null aad");
     if (k->nkeys > 1 && !b->key_idx) return fail(TG_EINVAL, "key table needs key_idx");
-    if (k->alg == TG_AES_GCM && b->key_idx)
-        return fail(TG_EINVAL, "AES-GCM key tables are not supported yet");
+    if (k->nkeys == 1 && b->key_idx) return fail(TG_EINVAL, "key_idx given for a single key");
     int rc = select_device(k);
     if (rc) return rc;
     hipStream_t s = static_cast<hipStream_t>(stream);  // NULL = the null stream
@@ -295,7 +298,6 @@ int tg_key_create(int alg, const uint8_t* keys, size_t keylen, size_t nkeys, tg_
     *out = nullptr;
     if (alg == TG_AES_GCM) {
         if (keylen != 16 && keylen != 32) return fail(TG_EKEYLEN, "AES-GCM key must be 16 or 32 bytes");
-        if (nkeys != 1) return fail(TG_EINVAL, "AES-GCM key tables are not supported yet");
     } else if (alg == TG_CHACHA20_POLY1305) {
         if (keylen != 32) return fail(TG_EKEYLEN, "Key must be 256 bit long");
     } else {
@@ -315,7 +317,38 @@ int tg_key_create(int alg, const uint8_t* keys, size_t keylen, size_t nkeys, tg_
         delete k;
         return fail(TG_EHIP, "hipStreamCreate: %s", hipGetErrorString(e));
     }
-    if (alg == TG_AES_GCM) {
+    if (alg == TG_AES_GCM && nkeys > 1) {
+        tg::GcmTableKey* hk = new (std::nothrow) tg::GcmTableKey[nkeys];
+        if (!hk) rc = fail(TG_ENOMEM, "out of host memory");
+        if (!rc) {
+            const HostAes& aes = host_aes();
+            for (size_t i = 0; i < nkeys; ++i) {
+                uint8_t rk[240] = {0};
+                const int nr = aes.expand(keys + keylen * i, keylen, rk);
+                memset(&hk[i], 0, sizeof(hk[i]));
+                for (int w = 0; w < 4 * (nr + 1); ++w) hk[i].rk[w] = le32(rk + 4 * w);
+                k->rounds = nr;
+                uint8_t zero[16] = {0}, h[16];
+                aes.encrypt(rk, nr, zero, h);                 // H = E_K(0^128)
+                for (int w = 0; w < 4; ++w) {                 // normal order: per-byte bit reversal
+                    uint32_t v = 0;
+                    for (int bt = 0; bt < 4; ++bt) {
+                        uint8_t x = h[4 * w + bt], r = 0;
+                        for (int t = 0; t < 8; ++t) r = (uint8_t)(r | (((x >> t) & 1) << (7 - t)));
+                        v |= (uint32_t)r << (8 * bt);
+                    }
+                    hk[i].hn[w] = v;
+                }
+                memset(rk, 0, sizeof(rk));
+            }
+            const size_t bytes = sizeof(tg::GcmTableKey) * nkeys;
+            e = hipMalloc(&k->dev_key, bytes);
+            if (e == hipSuccess) e = hipMemcpy(k->dev_key, hk, bytes, hipMemcpyHostToDevice);
+            if (e != hipSuccess) rc = fail(TG_EHIP, "key upload: %s", hipGetErrorString(e));
+            memset(hk, 0, sizeof(tg::GcmTableKey) * nkeys);
+            delete[] hk;
+        }
+    } else if (alg == TG_AES_GCM) {
         tg::GcmKeyDev* hk = new (std::nothrow) tg::GcmKeyDev();
         if (!hk) rc = fail(TG_ENOMEM, "out of host memory");
         if (!rc) {
@@ -364,7 +397,9 @@ int tg_key_destroy(tg_key* k) {
     if (k->stream) (void)hipStreamSynchronize(k->stream);
     if (k->dev_key) {
         // scrub key material before release
-        size_t bytes = k->alg == TG_AES_GCM ? sizeof(tg::GcmKeyDev) : sizeof(tg::ChachaKeyDev) * k->nkeys;
+        size_t bytes = k->alg != TG_AES_GCM ? sizeof(tg::ChachaKeyDev) * k->nkeys
+                       : k->nkeys > 1   ? sizeof(tg::GcmTableKey) * k->nkeys
+                                        : sizeof(tg::GcmKeyDev);
         (void)hipMemset(k->dev_key, 0, bytes);
         (void)hipFree(k->dev_key);
     }

@@ -24,6 +24,13 @@ struct GcmKeyDev {
     uint4 ghash[kGhashEntries];
 };
 
+// One entry of an AES-GCM key table (many sessions in one batch): the round
+// keys and H = E_K(0) in normal polynomial order (see GhashClmul).
+struct GcmTableKey {
+    uint32_t rk[60];
+    uint32_t hn[4];
+};
+
 struct ChachaKeyDev {
     uint32_t k[8];         // key as LE words (chacha.py:101, _bytearray_to_words)
 };
@@ -104,6 +111,8 @@ __device__ __forceinline__ uint4 mask_tail(uint4 v, uint32_t n) {
 // Launchers implemented in the kernel files (host side).
 int tg_launch_gcm(const tg::GcmKeyDev* key, int rounds, const tg_batch& b, bool open,
                   hipStream_t s);
+int tg_launch_gcm_table(const tg::GcmTableKey* keys, int rounds, const tg_batch& b, bool open,
+                        hipStream_t s);
 int tg_launch_chacha(const tg::ChachaKeyDev* keys, const tg_batch& b, bool open, hipStream_t s);
 int tg_launch_nonces(int mode, const uint8_t* iv_host, uint64_t seq0, uint64_t n, uint8_t* out,
                      hipStream_t s);
