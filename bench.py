@@ -95,7 +95,13 @@ def main():
     ap.add_argument("--e2e", action="store_true", help="also time the host<->device path")
     ap.add_argument("--record-align", type=int, default=128,
                     help="byte alignment of each sealed record (ct||tag) in the packed batch")
+    ap.add_argument("--config", default="headline", choices=["headline", "c4", "c5"],
+                    help="headline = BASELINE configs[1]+[2] (the metric); c4 = configs[3] "
+                         "(AES-256-GCM, 65536 keys, Zipf lengths); c5 = configs[4] (TLS 1.3 "
+                         "AES-128-GCM seal, 16385-byte inner plaintext, seq-sharded)")
     args = ap.parse_args()
+    if args.config == "c4":
+        return run_config4(args)
 
     import torch
     import torch.distributed as dist
@@ -227,6 +233,84 @@ def main():
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
+    if not ok:
+        sys.exit(3)
+
+
+def run_config4(args):
+    """BASELINE configs[3]: AES-256-GCM, 65 536 independent session keys
+    (PCG64 0x7716), 2^20 records with Zipf(1.2) lengths 64 B-16 KiB (PCG64
+    0x7717), TLS 1.2 AAD seq||0x17||0x0303||len and nonce iv4||seq.  Records
+    are packed in descending length order (the batch planner's choice: lanes of
+    a wavefront then carry similar lengths).  Reports payload GiB/s of seal and
+    of open, and the byte-weighted mean length."""
+    import numpy as np
+    import torch
+    import tlsgpu
+    torch.cuda.set_device(int(os.environ.get("LOCAL_RANK", "0")))
+    n, nkeys = args.records, 65536
+    rk = np.random.default_rng(0x7716)
+    keys = rk.integers(0, 256, (nkeys, 32), dtype=np.uint8)
+    key_idx = rk.integers(0, nkeys, n).astype(np.uint32)
+    rl = np.random.default_rng(0x7717)
+    lens = np.clip(64 * rl.zipf(1.2, n), 64, 16384).astype(np.int64)
+    order = np.argsort(-lens, kind="stable")
+    lens, key_idx = lens[order], key_idx[order]
+    seq = order.astype(np.uint64)           # record identity = its original seq number
+    in_sz = (lens + 15) // 16 * 16
+    out_sz = (lens + 16 + 15) // 16 * 16
+    in_off = np.concatenate([[0], np.cumsum(in_sz)[:-1]]).astype(np.int64)
+    out_off = np.concatenate([[0], np.cumsum(out_sz)[:-1]]).astype(np.int64)
+    aad = np.zeros((n, 13), dtype=np.uint8)
+    aad[:, :8] = seq[:, None].view(np.uint8).reshape(n, 8)[:, ::-1]
+    aad[:, 8], aad[:, 9], aad[:, 10] = 0x17, 3, 3
+    aad[:, 11], aad[:, 12] = lens >> 8, lens & 0xff
+    nonce = np.zeros((n, 12), dtype=np.uint8)
+    nonce[:, :4] = rk.integers(0, 256, 4, dtype=np.uint8)
+    nonce[:, 4:] = aad[:, :8]
+    d = lambda a: torch.from_numpy(np.ascontiguousarray(a)).cuda()  # noqa: E731
+    total_in, total_out = int(in_sz.sum()), int(out_sz.sum())
+    g = torch.Generator(device="cuda").manual_seed(0x7717)
+    inp = torch.randint(0, 256, (total_in,), dtype=torch.uint8, device="cuda", generator=g)
+    sealed = torch.empty(total_out, dtype=torch.uint8, device="cuda")
+    back = torch.empty_like(inp)
+    status = torch.zeros(n, dtype=torch.uint8, device="cuda")
+    d_lens, d_in_off, d_out_off = d(lens.astype(np.int32)), d(in_off), d(out_off)
+    d_aad, d_nonce, d_kidx = d(aad.reshape(-1)), d(nonce.reshape(-1)), d(key_idx.view(np.int32))
+    table = tlsgpu.KeyTable("aesgcm", [bytes(k) for k in keys])
+    sb = tlsgpu.make_batch(n, inp, sealed, d_nonce, aad=d_aad, lens=d_lens, in_off=d_in_off,
+                           out_off=d_out_off, aad_stride=13, fixed_aad_len=13, key_idx=d_kidx)
+    ob = tlsgpu.make_batch(n, sealed, back, d_nonce, aad=d_aad, lens=d_lens, in_off=d_out_off,
+                           out_off=d_in_off, aad_stride=13, fixed_aad_len=13, key_idx=d_kidx,
+                           status=status)
+    stream = torch.cuda.current_stream()
+    for _ in range(args.warmup):
+        tlsgpu.seal_batch(table, sb, stream)
+        tlsgpu.open_batch(table, ob, stream)
+    ms = {"seal": [], "open": []}
+    for _ in range(args.steps):
+        for op, fn, b in (("seal", tlsgpu.seal_batch, sb), ("open", tlsgpu.open_batch, ob)):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(stream)
+            fn(table, b, stream)
+            e1.record(stream)
+            ms[op].append((e0, e1))
+    torch.cuda.synchronize()
+    ok = int(status.sum().item()) == n and torch.equal(back, inp)
+    payload = float(lens.sum())
+    res = {}
+    for op, lst in ms.items():
+        t = sum(a.elapsed_time(b) for a, b in lst) / len(lst)
+        res[op] = {"ms": round(t, 3), "payload_GiBps": round(payload / (t / 1e3) / 2 ** 30, 1)}
+    line = {"metric": "GiB/s device-resident record seal/open, AES-256-GCM, 65536 keys, "
+                      "Zipf 64B-16KiB (BASELINE configs[3])",
+            "value": round(2 * payload / ((res["seal"]["ms"] + res["open"]["ms"]) / 1e3) / 2 ** 30, 2),
+            "unit": "GiB/s", "n_gpus": 1, "steps": args.steps, "warmup": args.warmup,
+            "dtype": "u8", "data": "synthetic", "records": n, "keys": nkeys,
+            "mean_len": round(float(lens.mean()), 1),
+            "byte_weighted_mean_len": round(float((lens * lens).sum() / lens.sum()), 1),
+            "per_op": res, "verified": bool(ok)}
+    print(json.dumps(line), flush=True)
     if not ok:
         sys.exit(3)
 
