@@ -174,16 +174,13 @@ def main():
 
     # correctness of the timed work (not timed): every record authentic, round trip exact
     ok = int(status.sum().item()) == n and torch.equal(back, inp)
-    counters = torch.tensor([float(n * args.steps * len(kinds)),
-                             float(n * L * args.steps * len(kinds)),
-                             float(n - int(status.sum().item())), elapsed], dtype=torch.float64,
-                            device=dev)
-    if world > 1:
-        tmax = counters[3:4].clone()
-        dist.all_reduce(counters, op=dist.ReduceOp.SUM)
-        dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
-        elapsed = float(tmax.item())
-    payload_bytes = float(counters[1].item())
+    # the only collective: counters summed and the timed span max-reduced (RCCL)
+    from tlsgpu.distributed import reduce_counters
+    nfail = n - int(status.sum().item())
+    sums, elapsed = reduce_counters(torch, dist, [n * args.steps * len(kinds),
+                                                  n * L * args.steps * len(kinds), nfail],
+                                    elapsed, device=dev)
+    payload_bytes = sums[1]
     per_kernel = {}
     for (a, op), lst in ev.items():
         ms = sum(e0.elapsed_time(e1) for e0, e1 in lst) / len(lst)
@@ -224,7 +221,7 @@ def main():
                          "frac": round(dom_achieved / HBM_PEAK_GBS, 4), "traffic": None,
                          "bytes_per_record": algorithmic_bytes(1, L, dom_op)},
             "verified": bool(ok),
-            "auth_failures": int(counters[2].item()),
+            "auth_failures": int(sums[2]),
         }
         if e2e:
             line["end_to_end"] = e2e
