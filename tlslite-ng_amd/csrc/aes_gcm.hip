@@ -20,6 +20,7 @@
 // Counter blocks are nonce || be32(2 + j); the reference's 128-bit
 // increment equals this 32-bit one because a record has < 2^28 blocks.
 #include <cstdlib>
+#include <type_traits>
 
 #include "common.h"
 
@@ -224,6 +225,59 @@ struct GhashTables {  // single key: the 8-bit tables staged in LDS; y in block 
     __device__ __forceinline__ uint4 finish(uint4 y) const { return y; }
 };
 
+// Bank-conflict-free variant.  Tables in row layout, entry (j, b) at
+// b * 256 + j * 16, so the 16-byte bank slot of a lookup is its table j.  Lane
+// l walks the tables starting at j = l % 16: at step t it looks up table
+// (t + l) % 16 with byte (t + l) % 16 of y, so the 16 lanes of every
+// ds_read_b128 group hit 16 different slots whatever the data.  y is rotated
+// by l % 16 bytes once per multiply (word rotation by two selects, byte
+// rotation by v_alignbit), after which byte t of the rotated value is static;
+// each address is one v_perm_b32 of (rotated word, lane's table-offset bytes).
+struct GhashTablesRot {
+    uint32_t r2, r1;   // lane & 8, lane & 4: word-rotation steps
+    uint32_t s8;       // 8 * (lane & 3): byte rotation in bits
+    uint32_t jt[4];    // byte t%4 of jt[t/4] = ((t + lane) % 16) * 16
+    __device__ __forceinline__ void init(uint32_t lane) {
+        const uint32_t l16 = lane & 15;
+        r2 = l16 & 8;
+        r1 = l16 & 4;
+        s8 = 8 * (l16 & 3);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            uint32_t v = 0;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) v |= (((l16 + 4 * q + k) & 15u) << 4) << (8 * k);
+            jt[q] = v;
+        }
+    }
+    __device__ __forceinline__ uint4 mul(uint4 y) const {
+        uint32_t u0 = y.x, u1 = y.y, u2 = y.z, u3 = y.w;
+        if (r2) { uint32_t t = u0; u0 = u2; u2 = t; t = u1; u1 = u3; u3 = t; }
+        if (r1) { uint32_t t = u0; u0 = u1; u1 = u2; u2 = u3; u3 = t; }
+        const uint32_t v[4] = {__builtin_amdgcn_alignbit(u1, u0, s8),
+                               __builtin_amdgcn_alignbit(u2, u1, s8),
+                               __builtin_amdgcn_alignbit(u3, u2, s8),
+                               __builtin_amdgcn_alignbit(u0, u3, s8)};
+        uint4 e[16];
+#pragma unroll
+        for (int t = 0; t < 16; ++t) {
+            // byte 1 <- v[t/4] byte t%4 (the row b), byte 0 <- jt[t/4] byte t%4
+            const uint32_t sel = 0x0c0c0000u | ((4u + (t & 3)) << 8) | (uint32_t)(t & 3);
+            e[t] = lds_u128(__builtin_amdgcn_perm(v[t >> 2], jt[t >> 2], sel));
+        }
+        uint4 z = xor4_3(e[0], e[1], e[2]);
+        z = xor4_3(z, e[3], e[4]);
+        z = xor4_3(z, e[5], e[6]);
+        z = xor4_3(z, e[7], e[8]);
+        z = xor4_3(z, e[9], e[10]);
+        z = xor4_3(z, e[11], e[12]);
+        z = xor4_3(z, e[13], e[14]);
+        return xor4(z, e[15]);
+    }
+    __device__ __forceinline__ uint4 update(uint4 y, uint4 blk) const { return mul(xor4(y, blk)); }
+    __device__ __forceinline__ uint4 finish(uint4 y) const { return y; }
+};
+
 // ---- table-free GHASH for key tables -----------------------------------
 // A key table cannot stage 64 KiB of GHASH tables per session, so each lane
 // multiplies by its own H with a carry-less multiply built from integer
@@ -399,12 +453,13 @@ __device__ __forceinline__ void gcm_record(const tg_batch& b, uint64_t i, uint32
 }
 
 
-template <int NR, bool OPEN, int G, int THREADS>
+template <int NR, bool OPEN, int G, int THREADS, bool ROT>
 __global__ __launch_bounds__(THREADS) void gcm_kernel(const GcmKeyDev* __restrict__ key,
                                                       tg_batch b) {
     uint4* lds = g_lds;
-    // stage the GHASH tables and the Te0/Te2 copies
-    for (int e = threadIdx.x; e < kGhashEntries; e += blockDim.x) lds[e] = key->ghash[e];
+    // stage the GHASH tables (ROT: row layout b * 16 + j) and the Te0/Te2 copies
+    for (int e = threadIdx.x; e < kGhashEntries; e += blockDim.x)
+        lds[ROT ? (e & 255) * 16 + (e >> 8) : e] = key->ghash[e];
     {
         uint32_t* te = reinterpret_cast<uint32_t*>(lds) + kTeBase / 4;
         for (int e = threadIdx.x; e < 256 * 64; e += blockDim.x) {
@@ -415,7 +470,8 @@ __global__ __launch_bounds__(THREADS) void gcm_kernel(const GcmKeyDev* __restric
     RkRegs<NR> rk;
 #pragma unroll
     for (int k = 0; k < 4 * (NR + 1); ++k) rk.w[k] = key->rk[k];
-    const GhashTables gh;
+    typename std::conditional<ROT, GhashTablesRot, GhashTables>::type gh;
+    if constexpr (ROT) gh.init(threadIdx.x & 63);
     __syncthreads();
 
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -455,18 +511,18 @@ __global__ __launch_bounds__(kMkThreads, 4) void gcm_table_kernel(const GcmTable
     gcm_record<NR, OPEN, G>(b, i, lane4, rk, gh);
 }
 
-template <int NR, bool OPEN, int G, int THREADS>
+template <int NR, bool OPEN, int G, int THREADS, bool ROT>
 int launch_v(const GcmKeyDev* key, const tg_batch& b, hipStream_t s) {
     static bool attr_set = false;
     if (!attr_set) {
-        if (hipFuncSetAttribute((const void*)gcm_kernel<NR, OPEN, G, THREADS>,
+        if (hipFuncSetAttribute((const void*)gcm_kernel<NR, OPEN, G, THREADS, ROT>,
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)kGcmLds) !=
             hipSuccess)
             return TG_EHIP;
         attr_set = true;
     }
     const uint64_t blocks = (b.n + THREADS - 1) / THREADS;
-    hipLaunchKernelGGL((gcm_kernel<NR, OPEN, G, THREADS>), dim3((unsigned)blocks), dim3(THREADS),
+    hipLaunchKernelGGL((gcm_kernel<NR, OPEN, G, THREADS, ROT>), dim3((unsigned)blocks), dim3(THREADS),
                        kGcmLds, s, key, b);
     return hipGetLastError() == hipSuccess ? TG_OK : TG_EHIP;
 }
@@ -485,10 +541,11 @@ int variant() {
 template <int NR, bool OPEN>
 int launch(const GcmKeyDev* key, const tg_batch& b, hipStream_t s) {
     switch (variant()) {
-        case 1: return launch_v<NR, OPEN, 4, 1024>(key, b, s);
-        case 2: return launch_v<NR, OPEN, 4, 512>(key, b, s);
-        case 3: return launch_v<NR, OPEN, 2, 512>(key, b, s);
-        default: return launch_v<NR, OPEN, 2, 1024>(key, b, s);
+        case 1: return launch_v<NR, OPEN, 4, 1024, false>(key, b, s);
+        case 2: return launch_v<NR, OPEN, 2, 1024, true>(key, b, s);
+        case 3: return launch_v<NR, OPEN, 1, 1024, true>(key, b, s);
+        case 4: return launch_v<NR, OPEN, 2, 512, true>(key, b, s);
+        default: return launch_v<NR, OPEN, 2, 1024, false>(key, b, s);
     }
 }
 
