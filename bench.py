@@ -102,18 +102,15 @@ def main():
     args = ap.parse_args()
     if args.config == "c4":
         return run_config4(args)
+    if args.config == "c5":
+        return run_config5(args)
 
     import torch
     import torch.distributed as dist
     import tlsgpu
     from vectors import tls13_aad
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local)
-    if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    world, rank, local = init_dist(torch, dist)
 
     n, L = args.records, args.len
     # sealed records are ct||tag (the wire form), packed at a stride rounded up
@@ -232,6 +229,80 @@ def main():
         dist.destroy_process_group()
     if not ok:
         sys.exit(3)
+
+
+def init_dist(torch, dist):
+    """One process per GPU (torch.distributed.run sets RANK/LOCAL_RANK/
+    WORLD_SIZE); backend "nccl" = RCCL over xGMI.  TLSGPU_DIST_BACKEND=gloo
+    and a device count below the world size are for rehearsal only."""
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    ndev = torch.cuda.device_count()
+    torch.cuda.set_device(local % ndev)
+    if world > 1:
+        backend = os.environ.get("TLSGPU_DIST_BACKEND", "nccl")
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local % ndev))
+        else:
+            dist.init_process_group(backend)
+    return world, rank, local
+
+
+def run_config5(args):
+    """BASELINE configs[4]: TLS 1.3 AES-128-GCM record seal, inner plaintext
+    L = 16385 (16384 application bytes + content type 0x17, recordlayer.py:
+    606-617), AAD 17 03 03 40 11, 2^20 records per GPU; rank g seals seq
+    [g*2^20, (g+1)*2^20) of one connection.  RCCL carries only the counters."""
+    import torch
+    import torch.distributed as dist
+    import tlsgpu
+    from tlsgpu.distributed import reduce_counters
+    from vectors import tls13_aad
+    world, rank, _ = init_dist(torch, dist)
+    n, L = args.records, 16385
+    SL = (L + TAG_LEN + args.record_align - 1) // args.record_align * args.record_align
+    IL = (L + 127) // 128 * 128
+    g = torch.Generator(device="cuda").manual_seed(0x7715 + rank)
+    inp = torch.randint(0, 256, (n * IL,), dtype=torch.uint8, device="cuda", generator=g)
+    inp.view(n, IL)[:, L - 1] = 0x17                       # TLS 1.3 inner content type
+    sealed = torch.empty(n * SL, dtype=torch.uint8, device="cuda")
+    nonces = torch.empty(12 * n, dtype=torch.uint8, device="cuda")
+    hrng = torch.Generator().manual_seed(0x7716)
+    iv = bytes(torch.randint(0, 256, (12,), dtype=torch.uint8, generator=hrng).tolist())
+    key = bytes(torch.randint(0, 256, (16,), dtype=torch.uint8, generator=hrng).tolist())
+    tlsgpu.make_nonces(iv, rank * n, n, nonces)
+    aad = torch.tensor(list(tls13_aad(L)), dtype=torch.uint8, device="cuda")
+    c = tlsgpu.HipAESGCM(bytearray(key))
+    b = tlsgpu.make_batch(n, inp, sealed, nonces, aad=aad, fixed_len=L, in_stride=IL,
+                          out_stride=SL, fixed_aad_len=AAD_LEN)
+    stream = torch.cuda.current_stream()
+    for _ in range(args.warmup):
+        tlsgpu.seal_batch(c, b, stream)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        tlsgpu.seal_batch(c, b, stream)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    sums, elapsed = reduce_counters(torch, dist, [n * args.steps, n * L * args.steps, 0],
+                                    time.perf_counter() - t0, device="cuda")
+    if rank == 0:
+        print(json.dumps({
+            "metric": "GiB/s device-resident TLS 1.3 AES-128-GCM record seal (BASELINE configs[4])",
+            "value": round(sums[1] / elapsed / 2 ** 30, 2), "unit": "GiB/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 3), "higher_is_better": True,
+            "scaling": "weak", "dtype": "u8", "data": "synthetic",
+            "config": {"workload": "configs[4]", "records_per_gpu": n, "inner_plaintext": L,
+                       "records_total": int(sums[0] / args.steps)}}), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
 
 
 def run_config4(args):
