@@ -11,6 +11,8 @@
 //     mac_data = aad || pad || ct || pad || le64 || le64 (:60-63) is never
 //     materialised;
 //   * Poly1305 runs in five 26-bit limbs with 32x32->64 multiply-adds.
+#include <cstdlib>
+
 #include "common.h"
 
 namespace tg {
@@ -245,8 +247,8 @@ __device__ __forceinline__ void tiled_blocks(WaveTile& t, uint32_t lane, uint32_
     }
 }
 
-template <bool OPEN, bool MULTIKEY>
-__global__ __launch_bounds__(kChachaThreads) void chacha_kernel(
+template <bool OPEN, bool MULTIKEY, int MINW>
+__global__ __launch_bounds__(kChachaThreads, MINW) void chacha_kernel(
     const ChachaKeyDev* __restrict__ keys, tg_batch b) {
     __shared__ WaveTile tiles[kWavesPerGroup];
     const uint64_t i_raw = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -337,12 +339,32 @@ __global__ __launch_bounds__(kChachaThreads) void chacha_kernel(
     }
 }
 
-template <bool OPEN, bool MULTIKEY>
-int launch(const ChachaKeyDev* keys, const tg_batch& b, hipStream_t s) {
+template <bool OPEN, bool MULTIKEY, int MINW>
+int launch_w(const ChachaKeyDev* keys, const tg_batch& b, hipStream_t s) {
     const uint64_t blocks = (b.n + kChachaThreads - 1) / kChachaThreads;
-    hipLaunchKernelGGL((chacha_kernel<OPEN, MULTIKEY>), dim3((unsigned)blocks),
+    hipLaunchKernelGGL((chacha_kernel<OPEN, MULTIKEY, MINW>), dim3((unsigned)blocks),
                        dim3(kChachaThreads), 0, s, keys, b);
     return hipGetLastError() == hipSuccess ? TG_OK : TG_EHIP;
+}
+
+// Occupancy variants (TLSGPU_CHACHA_VARIANT, measurement only): minimum
+// waves per SIMD requested from the register allocator.
+int chacha_variant() {
+    static int v = -1;
+    if (v < 0) {
+        const char* e = getenv("TLSGPU_CHACHA_VARIANT");
+        v = e ? atoi(e) : 0;
+    }
+    return v;
+}
+
+template <bool OPEN, bool MULTIKEY>
+int launch(const ChachaKeyDev* keys, const tg_batch& b, hipStream_t s) {
+    switch (chacha_variant()) {
+        case 1: return launch_w<OPEN, MULTIKEY, 5>(keys, b, s);
+        case 2: return launch_w<OPEN, MULTIKEY, 6>(keys, b, s);
+        default: return launch_w<OPEN, MULTIKEY, 1>(keys, b, s);
+    }
 }
 
 // RecordLayer._getNonce (recordlayer.py:522-534) for a run of sequence numbers.
