@@ -120,6 +120,54 @@ int tg_open_batch(tg_key* k, const tg_batch* b, void* stream);
 int tg_make_nonces(int mode, const uint8_t* iv, size_t ivlen, uint64_t seq0,
                    uint64_t n, uint8_t* out, void* stream);
 
+/* TLS record framing on the device -- the callers either side of the AEAD in
+ * tlslite/recordlayer.py: _getNonce (:522-534), _encryptThenSeal (:536-565,
+ * AAD, TLS 1.2 AES-GCM explicit nonce), sendRecord (:606-617, TLS 1.3 inner
+ * content type + zero padding, 5-byte header), _decryptAndUnseal (:780-824,
+ * publicly-invalid checks) and _tls13_de_pad (:863-884).  Record i has
+ * sequence number seq0 + i.  All arrays are DEVICE pointers.
+ *   seal: fragment data + data_off[i], data_len[i] bytes, content type
+ *         ctype[i]; TLS 1.3 appends ctype[i] and pad_len[i] zero bytes IN
+ *         PLACE after the fragment (the data buffer needs that much slack),
+ *         then writes the whole record (header || [explicit nonce] || ct ||
+ *         tag) at wire + wire_off[i] and its size to wire_len[i].
+ *   open: wire record (header included) at wire + wire_off[i], wire_len[i]
+ *         bytes; plaintext goes to data + data_off[i] (room for the inner
+ *         plaintext), its length to data_len[i], the (inner) content type to
+ *         ctype[i], and a TG_REC_* code to status[i].
+ * For the vector path place records so the payload after the header (and
+ * TLS 1.2 AES-GCM explicit nonce) is 16-byte aligned. */
+#define TG_TLS12 0x0303
+#define TG_TLS13 0x0304
+#define TG_REC_OK 0
+#define TG_REC_BAD_MAC 1        /* TLSBadRecordMAC (recordlayer.py:822-823) */
+#define TG_REC_TRUNCATED 2      /* "Truncated nonce" / "Truncated tag" (:788-789, :797-799) */
+#define TG_REC_LENGTH 3         /* "Length mismatch" (:816-817) */
+#define TG_REC_BAD_TYPE 4       /* TLSUnexpectedMessage, encrypted non-app-data (:809-812) */
+#define TG_REC_BAD_VERSION 5    /* TLSIllegalParameterException (:813-815) */
+#define TG_REC_NO_CONTENT_TYPE 6 /* malformed inner plaintext (:880-882) */
+
+typedef struct tg_records {
+    uint64_t n;
+    uint32_t version;           /* TG_TLS12 or TG_TLS13 */
+    uint32_t fixed_iv_len;      /* 4 (TLS 1.2 AES-GCM) or 12 */
+    uint8_t fixed_iv[12];
+    uint32_t reserved;
+    uint64_t seq0;
+    uint8_t* data;
+    const uint64_t* data_off;
+    uint32_t* data_len;
+    uint8_t* ctype;
+    const uint32_t* pad_len;    /* seal, TLS 1.3 only; NULL = no padding */
+    uint8_t* wire;
+    const uint64_t* wire_off;
+    uint32_t* wire_len;
+    uint8_t* status;            /* open */
+} tg_records;
+
+int tg_seal_records(tg_key* k, const tg_records* r, void* stream);
+int tg_open_records(tg_key* k, const tg_records* r, void* stream);
+
 /* Device memory helpers so a ctypes host needs no other GPU runtime. */
 int tg_malloc(void** p, size_t bytes);
 int tg_free(void* p);

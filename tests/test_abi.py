@@ -60,6 +60,21 @@ def test_struct_layout_matches_c(tmp_path):
         assert getattr(_lib.TgBatch, name).offset == off, name
 
 
+def test_records_struct_layout_matches_c(tmp_path):
+    from tlsgpu import _lib
+    names = [f[0] for f in _lib.TgRecords._fields_]
+    body = "".join('printf("%%zu\\n", offsetof(tg_records, %s));\n' % c for c in names)
+    src = tmp_path / "layout.c"
+    src.write_text('#include <stdio.h>\n#include <stddef.h>\n#include "tlsgpu.h"\n'
+                   'int main(void){printf("%%zu\\n", sizeof(tg_records));\n%sreturn 0;}\n' % body)
+    exe = tmp_path / "layout"
+    subprocess.check_call(["gcc", "-I", os.path.join(ROOT, "include"), str(src), "-o", str(exe)])
+    out = [int(x) for x in subprocess.check_output([str(exe)]).split()]
+    assert out[0] == ctypes.sizeof(_lib.TgRecords)
+    for name, off in zip(names, out[1:]):
+        assert getattr(_lib.TgRecords, name).offset == off, name
+
+
 def test_key_length_errors_match_reference():
     from tlsgpu import HipAESGCM, HipCHACHA20_POLY1305
     with pytest.raises(AssertionError):        # aesgcm.py:37-38

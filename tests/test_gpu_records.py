@@ -1,0 +1,144 @@
+"""GPU: device record framing (tg_seal_records / tg_open_records) against the
+reference RecordLayer's wire bytes (tests/golden/records.json) and the
+framing oracle (oracle/records.py)."""
+import hashlib
+
+import numpy as np
+import pytest
+
+from vectors import detbytes, load
+
+pytestmark = pytest.mark.gpu
+
+CASES = load("records.json")
+
+
+@pytest.fixture(scope="module")
+def torch():
+    import torch as t
+    if not t.cuda.is_available():
+        pytest.fail("GPU tests need a visible MI355X")
+    return t
+
+
+@pytest.fixture(scope="module")
+def tg(torch):
+    import tlsgpu
+    return tlsgpu
+
+
+def _key(tg, alg, key):
+    return tg.HipCHACHA20_POLY1305(bytearray(key)) if alg.startswith("chacha") else \
+        tg.HipAESGCM(bytearray(key))
+
+
+def _hdr(version, alg):
+    return 5 + (8 if version == "tls12" and not alg.startswith("chacha") else 0)
+
+
+def _layout(lens, pads, hdr, aligned):
+    """data offsets (16-aligned, with slack for ctype + padding) and wire
+    offsets (payload 16-aligned if ``aligned``, else packed back to back)."""
+    data_off, wire_off, d, w = [], [], 0, 0
+    for L, p in zip(lens, pads):
+        data_off.append(d)
+        d += (L + 1 + p + 16 + 15) // 16 * 16
+        if aligned:
+            w = (w + hdr + 15) // 16 * 16 - hdr
+        wire_off.append(w)
+        w += hdr + L + 1 + p + 16
+    return np.array(data_off, np.int64), np.array(wire_off, np.int64), d + 16, w + 64
+
+
+def _run(torch, tg, version, alg, key, iv, seq0, ctypes_, datas, pads, aligned, tamper=None):
+    n = len(datas)
+    lens = [len(x) for x in datas]
+    hdr = _hdr(version, alg)
+    data_off, wire_off, dsz, wsz = _layout(lens, pads, hdr, aligned)
+    host = np.zeros(dsz, np.uint8)
+    for o, x in zip(data_off, datas):
+        host[o:o + len(x)] = np.frombuffer(bytes(x), np.uint8)
+    dev = lambda a: torch.from_numpy(np.ascontiguousarray(a)).cuda()  # noqa: E731
+    data = dev(host)
+    d_off, w_off = dev(data_off), dev(wire_off)
+    d_len = dev(np.array(lens, np.int32))
+    ctype = dev(np.array(ctypes_, np.uint8))
+    pad = dev(np.array(pads, np.int32))
+    wire = torch.zeros(wsz, dtype=torch.uint8, device="cuda")
+    w_len = torch.zeros(n, dtype=torch.int32, device="cuda")
+    v = tg.TLS13 if version == "tls13" else tg.TLS12
+    k = _key(tg, alg, key)
+    tg.seal_records(k, v, iv, seq0, n, data, d_off, d_len, ctype, wire, w_off, w_len,
+                    pad_len=pad if version == "tls13" else None)
+    torch.cuda.synchronize()
+    wh, wl = wire.cpu().numpy(), w_len.cpu().numpy()
+    wires = [wh[o:o + l].tobytes() for o, l in zip(wire_off, wl)]
+    # open them back into a fresh data buffer
+    if tamper:
+        for i, fn in tamper.items():
+            nb = fn(wires[i])
+            wh[wire_off[i]:wire_off[i] + len(nb)] = np.frombuffer(nb, np.uint8)
+            wl[i] = len(nb)
+    wire2 = dev(wh)
+    w_len2 = dev(wl.astype(np.int32))
+    out = torch.zeros(dsz, dtype=torch.uint8, device="cuda")
+    o_len = torch.zeros(n, dtype=torch.int32, device="cuda")
+    o_ct = torch.zeros(n, dtype=torch.uint8, device="cuda")
+    st = torch.full((n,), 255, dtype=torch.uint8, device="cuda")
+    tg.open_records(k, v, iv, seq0, n, wire2, w_off, w_len2, out, d_off, o_len, o_ct, st)
+    torch.cuda.synchronize()
+    oh = out.cpu().numpy()
+    opened = [(int(s), int(c), oh[o:o + l].tobytes()) for s, c, o, l in
+              zip(st.cpu().numpy(), o_ct.cpu().numpy(), data_off, o_len.cpu().numpy())]
+    return wires, opened
+
+
+@pytest.mark.parametrize("ci", range(len(CASES)))
+@pytest.mark.parametrize("aligned", [True, False])
+def test_reference_wire_bytes(torch, tg, ci, aligned):
+    c = CASES[ci]
+    recs = c["records"]
+    datas = [bytes(detbytes("rec-%d-%d" % (s, r["len"]), r["len"])) for s, r in enumerate(recs)]
+    wires, opened = _run(torch, tg, c["version"], c["alg"], bytes.fromhex(c["key"]),
+                         bytes.fromhex(c["iv"]), c["seq0"], [r["ctype"] for r in recs], datas,
+                         [r["pad"] for r in recs], aligned)
+    for r, w, d, o in zip(recs, wires, datas, opened):
+        assert len(w) == r["wire_len"]
+        assert hashlib.sha256(w).hexdigest() == r["wire_sha256"], (c["version"], c["alg"])
+        assert o == (0, r["ctype"], d)
+
+
+@pytest.mark.parametrize("version,alg,klen,ivlen", [
+    ("tls13", "aes128gcm", 16, 12), ("tls13", "chacha20-poly1305", 32, 12),
+    ("tls12", "aes256gcm", 32, 4), ("tls12", "chacha20-poly1305", 32, 12)])
+def test_random_batch_vs_oracle_and_errors(torch, tg, version, alg, klen, ivlen):
+    from oracle import records as R
+    rng = np.random.default_rng(klen + ivlen)
+    n = 300
+    key, iv = rng.bytes(klen), rng.bytes(ivlen)
+    lens = list(rng.integers(0, 16385 - 300, n))
+    pads = [int(rng.integers(0, 256)) if version == "tls13" else 0 for _ in range(n)]
+    ctypes_ = [int(x) for x in rng.choice([21, 22, 23], n)]
+    datas = [rng.bytes(int(L)) for L in lens]
+    seq0 = 2 ** 40 + 3
+    tamper = {5: lambda w: w[:-1] + bytes([w[-1] ^ 1]),           # bad tag
+              7: lambda w: w[:21] if version == "tls13" else w[:12]}  # truncated
+    if version == "tls13":
+        tamper[9] = lambda w: b"\x16" + w[1:]                         # wrong outer type
+    wires, opened = _run(torch, tg, version, alg, key, iv, seq0, ctypes_, datas, pads, True,
+                         tamper=tamper)
+    for i in range(n):
+        want = R.seal_record(version, alg, key, iv, seq0 + i, ctypes_[i], datas[i], pads[i])
+        assert wires[i] == want, i
+        if i in tamper:
+            exp = R.open_record(version, alg, key, iv, seq0 + i, tamper[i](want))
+            assert opened[i][0] == exp[0] != 0, (i, opened[i][0], exp[0])
+        else:
+            assert opened[i] == (0, ctypes_[i], datas[i]), i
+
+
+def test_tls13_all_zero_inner_plaintext(torch, tg):
+    """ctype 0 with an empty fragment: _tls13_de_pad finds no content type."""
+    key, iv = bytes(16), bytes(12)
+    _, opened = _run(torch, tg, "tls13", "aes128gcm", key, iv, 0, [0, 23], [b"", b"x"], [3, 0], True)
+    assert opened[0][0] == 6 and opened[1] == (0, 23, b"x")

@@ -264,6 +264,75 @@ int batch(tg_key* k, const tg_batch* b, void* stream, bool open) {
     return TG_OK;
 }
 
+// Stream-ordered scratch for the record-framing calls.
+struct ScratchAlloc {
+    void* base = nullptr;
+    hipStream_t s = nullptr;
+    ~ScratchAlloc() {
+        if (base) (void)hipFreeAsync(base, s);
+    }
+};
+
+int records_scratch(uint64_t n, hipStream_t st, ScratchAlloc& a, tg::RecScratch& s) {
+    const size_t per = 8 + 8 + 4 + 12 + 16 + 4 + 1 + 1;
+    const size_t bytes = per * n + 64 + 64;
+    a.s = st;
+    HIP_TRY(hipMallocAsync(&a.base, bytes, st));
+    uint8_t* p = static_cast<uint8_t*>(a.base);
+    s.in_abs = reinterpret_cast<uint64_t*>(p); p += 8 * n;
+    s.out_abs = reinterpret_cast<uint64_t*>(p); p += 8 * n;
+    s.aad = p; p += 16 * n;
+    s.len = reinterpret_cast<uint32_t*>(p); p += 4 * n;
+    s.aad_len = reinterpret_cast<uint32_t*>(p); p += 4 * n;
+    s.nonce = p; p += 12 * n;
+    s.st = p; p += n;
+    s.aead_st = p; p += n;
+    p = reinterpret_cast<uint8_t*>((reinterpret_cast<uintptr_t>(p) + 63) & ~uintptr_t(63));
+    s.dummy = p;
+    HIP_TRY(hipMemsetAsync(s.dummy, 0, 32, st));
+    return TG_OK;
+}
+
+int records(tg_key* k, const tg_records* r, void* stream, bool seal) {
+    if (!k || !r) return fail(TG_EINVAL, "null argument");
+    if (r->n == 0) return TG_OK;
+    if (k->nkeys != 1) return fail(TG_EINVAL, "record framing needs a single-key handle");
+    if (r->version != TG_TLS12 && r->version != TG_TLS13)
+        return fail(TG_EINVAL, "version must be TG_TLS12 or TG_TLS13");
+    if (r->fixed_iv_len != 12 && !(r->fixed_iv_len == 4 && r->version == TG_TLS12))
+        return fail(TG_EINVAL, "fixed IV must be 12 bytes (or 4 for TLS 1.2)");
+    if (!r->data || !r->data_off || !r->data_len || !r->ctype || !r->wire || !r->wire_off ||
+        !r->wire_len || (!seal && !r->status))
+        return fail(TG_EINVAL, "null device array");
+    int rc = select_device(k);
+    if (rc) return rc;
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    ScratchAlloc alloc;
+    tg::RecScratch s;
+    if ((rc = records_scratch(r->n, st, alloc, s))) return rc;
+    const bool aes = k->alg == TG_AES_GCM;
+    if ((rc = tg_launch_records_prep(*r, seal, aes, s, st))) return fail(rc, "framing launch failed");
+    tg_batch b;
+    memset(&b, 0, sizeof(b));
+    b.n = r->n;
+    b.len = s.len;
+    b.nonce = s.nonce;
+    b.aad = s.aad;
+    b.aad_stride = 16;
+    b.aad_len = s.aad_len;
+    b.out_off = s.out_abs;          // absolute addresses: out base NULL
+    if (seal) {
+        b.in = r->data;
+        b.in_off = r->data_off;
+    } else {
+        b.in_off = s.in_abs;
+        b.status = s.aead_st;
+    }
+    if ((rc = launch(k, b, !seal, st))) return fail(rc, "AEAD launch failed");
+    if (!seal && (rc = tg_launch_records_finish(*r, s, st))) return fail(rc, "finish launch failed");
+    return TG_OK;
+}
+
 }  // namespace
 
 extern "C" {
@@ -434,6 +503,14 @@ int tg_open(tg_key* k, const uint8_t* nonce, size_t noncelen, const uint8_t* aad
 int tg_seal_batch(tg_key* k, const tg_batch* b, void* stream) { return batch(k, b, stream, false); }
 
 int tg_open_batch(tg_key* k, const tg_batch* b, void* stream) { return batch(k, b, stream, true); }
+
+int tg_seal_records(tg_key* k, const tg_records* r, void* stream) {
+    return records(k, r, stream, true);
+}
+
+int tg_open_records(tg_key* k, const tg_records* r, void* stream) {
+    return records(k, r, stream, false);
+}
 
 int tg_make_nonces(int mode, const uint8_t* iv, size_t ivlen, uint64_t seq0, uint64_t n,
                    uint8_t* out, void* stream) {

@@ -106,6 +106,19 @@ __device__ __forceinline__ uint4 mask_tail(uint4 v, uint32_t n) {
     return make_uint4(w[0], w[1], w[2], w[3]);
 }
 
+// Per-call device scratch of the record-framing entry points (records.hip).
+struct RecScratch {
+    uint64_t* in_abs;     // AEAD input address per record (open)
+    uint64_t* out_abs;    // AEAD output address per record
+    uint32_t* len;        // AEAD payload length (inner plaintext / ciphertext)
+    uint8_t* nonce;       // 12 B per record
+    uint8_t* aad;         // 16 B stride, 5 or 13 used
+    uint32_t* aad_len;
+    uint8_t* st;          // framing status from prep (open)
+    uint8_t* aead_st;     // AEAD open status
+    uint8_t* dummy;       // 32 zero bytes: AEAD input of publicly-invalid records
+};
+
 }  // namespace tg
 
 // Launchers implemented in the kernel files (host side).
@@ -114,5 +127,8 @@ int tg_launch_gcm(const tg::GcmKeyDev* key, int rounds, const tg_batch& b, bool 
 int tg_launch_gcm_table(const tg::GcmTableKey* keys, int rounds, const tg_batch& b, bool open,
                         hipStream_t s);
 int tg_launch_chacha(const tg::ChachaKeyDev* keys, const tg_batch& b, bool open, hipStream_t s);
+int tg_launch_records_prep(const tg_records& r, bool seal, bool aes, const tg::RecScratch& s,
+                           hipStream_t st);
+int tg_launch_records_finish(const tg_records& r, const tg::RecScratch& s, hipStream_t st);
 int tg_launch_nonces(int mode, const uint8_t* iv_host, uint64_t seq0, uint64_t n, uint8_t* out,
                      hipStream_t s);

@@ -9,5 +9,6 @@ from ._lib import TlsGpuError, device_count, load  # noqa: F401
 from .aead import HipAESGCM, HipCHACHA20_POLY1305  # noqa: F401
 from .batch import KeyTable, make_batch, make_nonces, open_batch, seal_batch  # noqa: F401
 from .cipherfactory import CIPHER_IMPLEMENTATIONS, createAESGCM, createCHACHA20  # noqa: F401
+from .records import TLS12, TLS13, open_records, seal_records  # noqa: F401
 
 __version__ = "0.1.0"

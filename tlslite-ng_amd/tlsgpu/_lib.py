@@ -25,7 +25,13 @@ TG_CHACHA20_POLY1305 = 1
 EXPORTS = ("tg_version", "tg_last_error", "tg_device_count", "tg_init", "tg_key_create",
            "tg_key_destroy", "tg_key_info", "tg_seal", "tg_open", "tg_seal_batch",
            "tg_open_batch", "tg_make_nonces", "tg_malloc", "tg_free", "tg_memcpy_h2d",
-           "tg_memcpy_d2h", "tg_stream_sync")
+           "tg_memcpy_d2h", "tg_stream_sync", "tg_seal_records", "tg_open_records")
+
+TG_TLS12 = 0x0303
+TG_TLS13 = 0x0304
+# per-record status of tg_open_records (include/tlsgpu.h TG_REC_*)
+REC_STATUS = {0: "ok", 1: "bad_record_mac", 2: "truncated", 3: "length_mismatch",
+              4: "unexpected_content_type", 5: "illegal_version", 6: "no_content_type"}
 
 
 class TgBatch(ctypes.Structure):
@@ -47,6 +53,27 @@ class TgBatch(ctypes.Structure):
         ("aad_stride", ctypes.c_uint64),
         ("aad_len", ctypes.c_void_p),
         ("key_idx", ctypes.c_void_p),
+        ("status", ctypes.c_void_p),
+    ]
+
+
+class TgRecords(ctypes.Structure):
+    """``struct tg_records`` (include/tlsgpu.h)."""
+    _fields_ = [
+        ("n", ctypes.c_uint64),
+        ("version", ctypes.c_uint32),
+        ("fixed_iv_len", ctypes.c_uint32),
+        ("fixed_iv", ctypes.c_uint8 * 12),
+        ("reserved", ctypes.c_uint32),
+        ("seq0", ctypes.c_uint64),
+        ("data", ctypes.c_void_p),
+        ("data_off", ctypes.c_void_p),
+        ("data_len", ctypes.c_void_p),
+        ("ctype", ctypes.c_void_p),
+        ("pad_len", ctypes.c_void_p),
+        ("wire", ctypes.c_void_p),
+        ("wire_off", ctypes.c_void_p),
+        ("wire_len", ctypes.c_void_p),
         ("status", ctypes.c_void_p),
     ]
 
@@ -85,6 +112,8 @@ def load():
     l.tg_seal_batch.argtypes = [p, ctypes.POINTER(TgBatch), p]
     l.tg_open_batch.argtypes = [p, ctypes.POINTER(TgBatch), p]
     l.tg_make_nonces.argtypes = [i, p, sz, u64, u64, p, p]
+    l.tg_seal_records.argtypes = [p, ctypes.POINTER(TgRecords), p]
+    l.tg_open_records.argtypes = [p, ctypes.POINTER(TgRecords), p]
     l.tg_malloc.argtypes = [ctypes.POINTER(ctypes.c_void_p), sz]
     l.tg_free.argtypes = [p]
     l.tg_memcpy_h2d.argtypes = [p, p, sz, p]
