@@ -59,6 +59,9 @@ OP_KERNEL(k_xor_sdwa, uint32_t, c + seed + threadIdx.x, asm volatile("v_xor_b32_
 OP_KERNEL(k_lshrrev, uint32_t, c + seed + threadIdx.x, ASM2("v_lshrrev_b32"))
 OP_KERNEL(k_and_b32, uint32_t, c + seed + threadIdx.x, ASM2("v_and_b32"))
 OP_KERNEL(k_xad_u32, uint32_t, c + seed + threadIdx.x, ASM3("v_xad_u32"))
+OP_KERNEL(k_pk_rot16, uint32_t, c + seed + threadIdx.x, asm volatile("v_pk_add_u16 %0, %1, 0 op_sel:[1,1] op_sel_hi:[0,0]" : "=v"(x[c]) : "v"(N1)))
+OP_KERNEL(k_pk_add_u16, uint32_t, c + seed + threadIdx.x, ASM2("v_pk_add_u16"))
+OP_KERNEL(k_cndmask, uint32_t, c + seed + threadIdx.x, asm volatile("v_cndmask_b32 %0, %0, %1, vcc" : "+v"(x[c]) : "v"(N1)))
 OP_KERNEL(k_add_u64, uint64_t, c + seed + threadIdx.x, asm volatile("v_lshl_add_u64 %0, %0, 0, %1" : "+v"(x[c]) : "v"(N1)))
 
 __global__ void k_mad_u64_u32(uint64_t* out, uint32_t seed) {
@@ -201,6 +204,9 @@ int main() {
     RUN(k_mad_u64_u32, uint64_t);
     RUN(k_add_u64, uint64_t);
     RUN(k_bitop3, uint32_t);
+    RUN(k_pk_rot16, uint32_t);
+    RUN(k_pk_add_u16, uint32_t);
+    RUN(k_cndmask, uint32_t);
     RUN(k_xor_sdwa, uint32_t);
     RUN(k_lshrrev, uint32_t);
     RUN(k_and_b32, uint32_t);
