@@ -4,7 +4,7 @@
  * TEST INFRASTRUCTURE ONLY (see aead_oracle.h).  Parity of this restatement
  * with the reference is pinned in tests/test_oracle_golden.py against
  *   - the reference's own known-answer vectors (unit_tests/
- *     test_tlslite_utils_{aesgcm,chacha20_poly1305,chacha,poly1305}.py), and
+ *     test_tlslite_utils_{aesgcm,aesccm,chacha20_poly1305,chacha,poly1305}.py), and
  *   - golden vectors produced by running the reference itself
  *     (tests/golden/make_golden.py -> tests/golden/ JSON files).
  *
@@ -497,6 +497,132 @@ int oracle_chacha_open(const uint8_t* key, size_t keylen, const uint8_t* nonce,
     return 1;
 }
 
+/* ------------------------------------------------------------------- CCM --
+ * AESCCM (aesccm.py:11-155, RFC 3610 with a 12-byte nonce, so L = 3).     */
+
+/* numberToByteArray(v, n) (cryptomath.py:210-225): big-endian, keeping the
+ * low n bytes when v does not fit. */
+static void put_be(uint8_t* p, uint64_t v, int n) {
+    for (int k = n - 1; k >= 0; --k, v >>= 8) p[k] = (uint8_t)v;
+}
+
+/* AESCCM._cbcmac_calc, aesccm.py:36-83: CBC-MAC with a zero IV over
+ * B_0 || enc(len(aad)) || aad || pad16 || msg || pad16. */
+static void ccm_cbcmac(const aes_ctx* c, size_t taglen, const uint8_t* nonce,
+                       const uint8_t* aad, size_t aadlen, const uint8_t* msg,
+                       size_t len, uint8_t mac[16]) {
+    uint8_t x[16], blk[16];
+    /* flags (:40-43), B_0 (:46) */
+    blk[0] = (uint8_t)(64 * (aadlen > 0) + 8 * ((taglen - 2) / 2) + (3 - 1));
+    memcpy(blk + 1, nonce, 12);
+    put_be(blk + 13, len, 3);
+    aes_encrypt(c, blk, x);
+    if (aadlen) {
+        /* length encoding (:48-58) then aad, zero-padded to a block (:63-67) */
+        uint8_t pre[10];
+        size_t np;
+        if (aadlen < 0xff00) {
+            put_be(pre, aadlen, 2); np = 2;
+        } else if ((uint64_t)aadlen < 0x100000000ull) {
+            pre[0] = 0xff; pre[1] = 0xfe; put_be(pre + 2, aadlen, 4); np = 6;
+        } else {
+            pre[0] = 0xff; pre[1] = 0xff; put_be(pre + 2, aadlen, 8); np = 10;
+        }
+        size_t total = np + aadlen;
+        for (size_t off = 0; off < total; off += 16) {
+            for (size_t k = 0; k < 16; ++k) {
+                size_t s = off + k;
+                uint8_t b = s < np ? pre[s] : (s < total ? aad[s - np] : 0);
+                blk[k] = (uint8_t)(x[k] ^ b);
+            }
+            aes_encrypt(c, blk, x);
+        }
+    }
+    for (size_t off = 0; off < len; off += 16) {   /* msg, zero-padded (:68-70) */
+        for (size_t k = 0; k < 16; ++k)
+            blk[k] = (uint8_t)(x[k] ^ (off + k < len ? msg[off + k] : 0));
+        aes_encrypt(c, blk, x);
+    }
+    memcpy(mac, x, 16);                               /* :78-83 (caller truncates) */
+}
+
+/* Python_AES_CTR from counter block s_j = 2 || nonce || be24(j): the
+ * reference's 128-bit increment (python_aes.py:101-107) from s_0. */
+static void ccm_ctr_block(const aes_ctx* c, const uint8_t* nonce, uint64_t j, uint8_t ks[16]) {
+    uint8_t a[16];
+    a[0] = 2;                                         /* flags = L - 1 (aesccm.py:99) */
+    memcpy(a + 1, nonce, 12);
+    a[13] = a[14] = a[15] = 0;
+    for (int k = 15; k >= 0 && j; --k) {              /* a += j, big-endian */
+        uint64_t v = (uint64_t)a[k] + (j & 0xff);
+        a[k] = (uint8_t)v;
+        j = (j >> 8) + (v >> 8);
+    }
+    aes_encrypt(c, a, ks);
+}
+
+static void ccm_ctr(const aes_ctx* c, const uint8_t* nonce, const uint8_t* in, size_t n,
+                    uint8_t* out) {
+    uint8_t ks[16];
+    for (size_t off = 0; off < n; off += 16) {
+        ccm_ctr_block(c, nonce, 1 + off / 16, ks);   /* S_1.. encrypt the message */
+        size_t m = n - off < 16 ? n - off : 16;
+        for (size_t k = 0; k < m; ++k) out[off + k] = (uint8_t)(in[off + k] ^ ks[k]);
+    }
+}
+
+/* AESCCM.seal, aesccm.py:85-113: out = ct || tag (len + taglen bytes). */
+static int ccm_seal_ctx(const aes_ctx* c, size_t taglen, const uint8_t* nonce,
+                        const uint8_t* aad, size_t aadlen, const uint8_t* pt, size_t len,
+                        uint8_t* out) {
+    uint8_t mac[16], s0[16];
+    ccm_cbcmac(c, taglen, nonce, aad, aadlen, pt, len, mac);
+    ccm_ctr_block(c, nonce, 0, s0);                   /* auth value = mac ^ E(S_0) */
+    ccm_ctr(c, nonce, pt, len, out);
+    for (size_t k = 0; k < taglen; ++k) out[len + k] = (uint8_t)(mac[k] ^ s0[k]);
+    return 0;
+}
+
+/* AESCCM.open, aesccm.py:115-149: decrypt, recompute the MAC over the
+ * plaintext, compare; 0 (None) on mismatch or when inlen < taglen. */
+static int ccm_open_ctx(const aes_ctx* c, size_t taglen, const uint8_t* nonce,
+                        const uint8_t* aad, size_t aadlen, const uint8_t* in, size_t inlen,
+                        uint8_t* pt) {
+    if (inlen < taglen) return 0;                     /* :120-123 */
+    size_t len = inlen - taglen;
+    uint8_t mac[16], s0[16];
+    ccm_ctr(c, nonce, in, len, pt);
+    ccm_cbcmac(c, taglen, nonce, aad, aadlen, pt, len, mac);
+    ccm_ctr_block(c, nonce, 0, s0);
+    uint8_t diff = 0;                                 /* received_mac != computed_mac (:145) */
+    for (size_t k = 0; k < taglen; ++k) diff |= (uint8_t)(mac[k] ^ s0[k] ^ in[len + k]);
+    if (diff) {
+        memset(pt, 0, len);
+        return 0;
+    }
+    return 1;
+}
+
+int oracle_ccm_seal(const uint8_t* key, size_t keylen, size_t taglen, const uint8_t* nonce,
+                    size_t noncelen, const uint8_t* aad, size_t aadlen,
+                    const uint8_t* pt, size_t len, uint8_t* out) {
+    aes_ctx c;
+    if ((keylen != 16 && keylen != 32) || (taglen != 8 && taglen != 16)) return -2;  /* :22-30 */
+    if (aes_setup(&c, key, keylen)) return -2;
+    if (noncelen != 12) return -1;                    /* :87-88 */
+    return ccm_seal_ctx(&c, taglen, nonce, aad, aadlen, pt, len, out);
+}
+
+int oracle_ccm_open(const uint8_t* key, size_t keylen, size_t taglen, const uint8_t* nonce,
+                    size_t noncelen, const uint8_t* aad, size_t aadlen,
+                    const uint8_t* in, size_t inlen, uint8_t* pt) {
+    aes_ctx c;
+    if ((keylen != 16 && keylen != 32) || (taglen != 8 && taglen != 16)) return -2;
+    if (aes_setup(&c, key, keylen)) return -2;
+    if (noncelen != 12) return -1;                    /* :117-118 */
+    return ccm_open_ctx(&c, taglen, nonce, aad, aadlen, in, inlen, pt);
+}
+
 /* ----------------------------------------------------------------- batch */
 typedef struct {
     int alg, op;
@@ -510,6 +636,7 @@ typedef struct {
 static void* batch_worker(void* arg) {
     batch_job* j = (batch_job*)arg;
     gcm_ctx g;
+    aes_ctx a;
     uint32_t cur_key = 0xffffffffu;
     for (size_t i = j->begin; i < j->end; ++i) {
         uint32_t ki = j->key_idx ? j->key_idx[i] : 0;
@@ -526,6 +653,14 @@ static void* batch_worker(void* arg) {
             }
             rc = j->op == 0 ? gcm_seal_ctx(&g, nonce, ad, j->aad_len[i], src, j->inlen[i], dst)
                             : gcm_open_ctx(&g, nonce, ad, j->aad_len[i], src, j->inlen[i], dst);
+        } else if (j->alg == 2 || j->alg == 3) {
+            size_t tl = j->alg == 2 ? 16 : 8;
+            if (ki != cur_key) {
+                if (aes_setup(&a, key, j->keylen)) { j->rc = -1; return NULL; }
+                cur_key = ki;
+            }
+            rc = j->op == 0 ? ccm_seal_ctx(&a, tl, nonce, ad, j->aad_len[i], src, j->inlen[i], dst)
+                            : ccm_open_ctx(&a, tl, nonce, ad, j->aad_len[i], src, j->inlen[i], dst);
         } else {
             rc = j->op == 0 ? oracle_chacha_seal(key, j->keylen, nonce, 12, ad, j->aad_len[i],
                                                  src, j->inlen[i], dst)

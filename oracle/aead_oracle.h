@@ -36,6 +36,16 @@ int oracle_gcm_open(const uint8_t* key, size_t keylen, const uint8_t* nonce,
                     size_t noncelen, const uint8_t* aad, size_t aadlen,
                     const uint8_t* in, size_t inlen, uint8_t* pt);
 
+/* AESCCM.seal/open (aesccm.py:85-149), taglen 16 (aes*ccm) or 8 (aes*ccm_8):
+ * out = ct || tag (len + taglen).  Conventions as the GCM pair; a rejected
+ * open zeroes pt. */
+int oracle_ccm_seal(const uint8_t* key, size_t keylen, size_t taglen, const uint8_t* nonce,
+                    size_t noncelen, const uint8_t* aad, size_t aadlen,
+                    const uint8_t* pt, size_t len, uint8_t* out);
+int oracle_ccm_open(const uint8_t* key, size_t keylen, size_t taglen, const uint8_t* nonce,
+                    size_t noncelen, const uint8_t* aad, size_t aadlen,
+                    const uint8_t* in, size_t inlen, uint8_t* pt);
+
 /* ChaCha20 keystream XOR (chacha.py:98-153), counter is the initial block. */
 int oracle_chacha20_xor(const uint8_t key[32], const uint8_t nonce[12],
                         uint32_t counter, const uint8_t* in, size_t len,
@@ -53,7 +63,8 @@ int oracle_chacha_open(const uint8_t* key, size_t keylen, const uint8_t* nonce,
                        const uint8_t* in, size_t inlen, uint8_t* pt);
 
 /* Batch form used for sampled parity checks and the CPU baseline.
- * alg: 0 = AES-GCM, 1 = ChaCha20-Poly1305.  op: 0 = seal, 1 = open.
+ * alg: 0 = AES-GCM, 1 = ChaCha20-Poly1305, 2 = AES-CCM, 3 = AES-CCM_8.
+ * op: 0 = seal, 1 = open.
  * keys: nkeys x keylen; key_idx may be NULL (all records use key 0).
  * Record i: input at in + in_off[i], inlen[i] bytes (open: ct||tag);
  * nonce at nonces + 12*i; aad at aad + aad_off[i], aad_len[i] bytes;

@@ -8,7 +8,8 @@ links nor calls it.
 Each function mirrors the object method of the reference it restates:
 ``gcm_seal``/``gcm_open`` = ``AESGCM.seal/open`` (tlslite/utils/aesgcm.py:101,126),
 ``chacha_seal``/``chacha_open`` = ``CHACHA20_POLY1305.seal/open``
-(tlslite/utils/chacha20_poly1305.py:48,68), including the error conventions
+(tlslite/utils/chacha20_poly1305.py:48,68), ``ccm_seal``/``ccm_open`` =
+``AESCCM.seal/open`` (tlslite/utils/aesccm.py:85,115), including the error conventions
 (``ValueError`` on a bad nonce, ``None`` on a rejected record).
 """
 import ctypes
@@ -41,6 +42,8 @@ def lib():
         l.oracle_gcm_open.argtypes = [p, sz, p, sz, p, sz, p, sz, p]
         l.oracle_chacha_seal.argtypes = [p, sz, p, sz, p, sz, p, sz, p]
         l.oracle_chacha_open.argtypes = [p, sz, p, sz, p, sz, p, sz, p]
+        l.oracle_ccm_seal.argtypes = [p, sz, sz, p, sz, p, sz, p, sz, p]
+        l.oracle_ccm_open.argtypes = [p, sz, sz, p, sz, p, sz, p, sz, p]
         l.oracle_aes_encrypt_block.argtypes = [p, sz, p, p]
         l.oracle_chacha20_xor.argtypes = [p, p, ctypes.c_uint32, p, sz, p]
         l.oracle_chacha20_xor.restype = ctypes.c_int
@@ -97,6 +100,32 @@ def chacha_open(key, nonce, ct, aad=b""):
     return _open(lib().oracle_chacha_open, key, nonce, ct, aad)
 
 
+def ccm_seal(key, nonce, pt, aad=b"", taglen=16):
+    key, aad, pt, nonce = bytes(key), bytes(aad), bytes(pt), bytes(nonce)
+    out = ctypes.create_string_buffer(len(pt) + taglen)
+    rc = lib().oracle_ccm_seal(key, len(key), taglen, nonce, len(nonce), aad, len(aad), pt,
+                               len(pt), out)
+    if rc == -1:
+        raise ValueError("Bad nonce length")
+    if rc == -2:
+        raise AssertionError("Bad key length")
+    return bytearray(out.raw)
+
+
+def ccm_open(key, nonce, ct, aad=b"", taglen=16):
+    key, aad, ct, nonce = bytes(key), bytes(aad), bytes(ct), bytes(nonce)
+    out = ctypes.create_string_buffer(max(len(ct) - taglen, 1))
+    rc = lib().oracle_ccm_open(key, len(key), taglen, nonce, len(nonce), aad, len(aad), ct,
+                               len(ct), out)
+    if rc == -1:
+        raise ValueError("Bad nonce length")
+    if rc == -2:
+        raise AssertionError("Bad key length")
+    if rc == 0:
+        return None
+    return bytearray(out.raw[:len(ct) - taglen])
+
+
 def aes_block(key, block):
     key, block = bytes(key), bytes(block)
     out = ctypes.create_string_buffer(16)
@@ -127,10 +156,10 @@ def batch(alg, op, keys, nonces, aad, aad_off, aad_len, inp, in_off, inlen,
           out_size, out_off, key_idx=None, nthreads=1):
     """Numpy batch form (see ``oracle_batch`` in aead_oracle.h).
 
-    ``alg``: "aesgcm" or "chacha"; ``op``: "seal" or "open".  Returns
-    ``(out, status)``; ``status`` is None for seal.
+    ``alg``: "aesgcm", "chacha", "aesccm" or "aesccm8"; ``op``: "seal" or
+    "open".  Returns ``(out, status)``; ``status`` is None for seal.
     """
-    a = {"aesgcm": 0, "chacha": 1}[alg]
+    a = {"aesgcm": 0, "chacha": 1, "aesccm": 2, "aesccm8": 3}[alg]
     o = {"seal": 0, "open": 1}[op]
     keys = np.ascontiguousarray(keys, dtype=np.uint8)
     keylen = keys.shape[-1] if keys.ndim > 1 else keys.size
