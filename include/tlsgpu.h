@@ -43,6 +43,10 @@ extern "C" {
 /* Algorithms (the reference's cipher .name values). */
 #define TG_AES_GCM 0          /* "aes128gcm" (16-byte key) / "aes256gcm" (32) */
 #define TG_CHACHA20_POLY1305 1 /* "chacha20-poly1305" (32-byte key) */
+#define TG_AES_CCM 2          /* "aes128ccm" / "aes256ccm": 16-byte tag
+                                 (aesccm.py:11-155, cipherfactory.py:102-121) */
+#define TG_AES_CCM_8 3        /* "aes128ccm_8" / "aes256ccm_8": 8-byte tag
+                                 (cipherfactory.py:123-142) */
 
 typedef struct tg_key tg_key;
 
@@ -62,12 +66,15 @@ int tg_key_create(int alg, const uint8_t* keys, size_t keylen, size_t nkeys,
 int tg_key_destroy(tg_key* k);
 int tg_key_info(const tg_key* k, int* alg, size_t* keylen, size_t* nkeys);
 
+/* Tag length of a key's algorithm: 16, or 8 for TG_AES_CCM_8.  Below, "T"
+ * is this length. */
+int tg_key_taglen(const tg_key* k);
 /* Per-record drop-in, HOST buffers (synchronous).
- * tg_seal: out receives ct || tag (len + 16 bytes) -- AESGCM.seal /
- *   CHACHA20_POLY1305.seal.
- * tg_open: in = ct || tag (inlen bytes); pt receives inlen - 16 bytes.
+ * tg_seal: out receives ct || tag (len + T bytes) -- AESGCM.seal /
+ *   CHACHA20_POLY1305.seal / AESCCM.seal.
+ * tg_open: in = ct || tag (inlen bytes); pt receives inlen - T bytes.
  *   Returns 1 when the tag verifies, 0 when the record is rejected (the
- *   reference's None: bad tag, or inlen < 16), negative on error.
+ *   reference's None: bad tag, or inlen < T), negative on error.
  *   On rejection pt is zeroed, never left holding unauthenticated bytes. */
 int tg_seal(tg_key* k, const uint8_t* nonce, size_t noncelen,
             const uint8_t* aad, size_t aadlen, const uint8_t* pt, size_t len,
@@ -78,9 +85,9 @@ int tg_open(tg_key* k, const uint8_t* nonce, size_t noncelen,
 
 /* Batch of records, DEVICE pointers.  Record i:
  *   payload  in  + (in_off  ? in_off[i]  : i * in_stride),  len[i] bytes
- *            (seal: plaintext; open: ciphertext, followed by its 16-byte tag)
+ *            (seal: plaintext; open: ciphertext, followed by its T-byte tag)
  *   output   out + (out_off ? out_off[i] : i * out_stride)
- *            (seal: ct || tag, len[i] + 16 bytes; open: pt, len[i] bytes)
+ *            (seal: ct || tag, len[i] + T bytes; open: pt, len[i] bytes)
  *   nonce    nonce + 12 * i (12 bytes)
  *   aad      aad + (aad_off ? aad_off[i] : i * aad_stride),
  *            aad_len ? aad_len[i] : fixed_aad_len bytes
@@ -88,7 +95,9 @@ int tg_open(tg_key* k, const uint8_t* nonce, size_t noncelen,
  *   status   open only: status[i] = 1 authentic / 0 rejected (pt zeroed)
  * len == NULL means every record is fixed_len bytes.  Offsets with 16-byte
  * alignment take the vector path; any alignment is accepted.
- * Records are independent; nothing is ordered between them. */
+ * Records are independent; nothing is ordered between them.  AES-CCM records
+ * must be shorter than 2^28 - 32 bytes (the 3-byte CCM counter; TLS records
+ * are at most 2^14 + 256). */
 typedef struct tg_batch {
     uint64_t n;
     const uint8_t* in;
@@ -115,14 +124,15 @@ int tg_open_batch(tg_key* k, const tg_batch* b, void* stream);
 /* Build per-record 12-byte nonces on the device from a connection's fixed IV
  * and sequence numbers, as RecordLayer._getNonce does (recordlayer.py:522-534):
  *   mode 0 (TLS 1.3 / RFC ChaCha): nonce_i = iv12 xor (0^4 || be64(seq0 + i))
- *   mode 1 (TLS 1.2 GCM, draft ChaCha): nonce_i = iv4 || be64(seq0 + i)
+ *   mode 1 (TLS 1.2 AES-GCM / AES-CCM, draft ChaCha):
+ *          nonce_i = iv4 || be64(seq0 + i)
  * out: device, 12 * n bytes. */
 int tg_make_nonces(int mode, const uint8_t* iv, size_t ivlen, uint64_t seq0,
                    uint64_t n, uint8_t* out, void* stream);
 
 /* TLS record framing on the device -- the callers either side of the AEAD in
  * tlslite/recordlayer.py: _getNonce (:522-534), _encryptThenSeal (:536-565,
- * AAD, TLS 1.2 AES-GCM explicit nonce), sendRecord (:606-617, TLS 1.3 inner
+ * AAD, TLS 1.2 AES-GCM / AES-CCM explicit nonce), sendRecord (:606-617, TLS 1.3 inner
  * content type + zero padding, 5-byte header), _decryptAndUnseal (:780-824,
  * publicly-invalid checks) and _tls13_de_pad (:863-884).  Record i has
  * sequence number seq0 + i.  All arrays are DEVICE pointers.
@@ -136,7 +146,7 @@ int tg_make_nonces(int mode, const uint8_t* iv, size_t ivlen, uint64_t seq0,
  *         plaintext), its length to data_len[i], the (inner) content type to
  *         ctype[i], and a TG_REC_* code to status[i].
  * For the vector path place records so the payload after the header (and
- * TLS 1.2 AES-GCM explicit nonce) is 16-byte aligned. */
+ * TLS 1.2 AES explicit nonce) is 16-byte aligned.  The tag is T bytes. */
 #define TG_TLS12 0x0303
 #define TG_TLS13 0x0304
 #define TG_REC_OK 0
@@ -150,7 +160,7 @@ int tg_make_nonces(int mode, const uint8_t* iv, size_t ivlen, uint64_t seq0,
 typedef struct tg_records {
     uint64_t n;
     uint32_t version;           /* TG_TLS12 or TG_TLS13 */
-    uint32_t fixed_iv_len;      /* 4 (TLS 1.2 AES-GCM) or 12 */
+    uint32_t fixed_iv_len;      /* 4 (TLS 1.2 AES-GCM / AES-CCM) or 12 */
     uint8_t fixed_iv[12];
     uint32_t reserved;
     uint64_t seq0;

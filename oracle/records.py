@@ -13,9 +13,17 @@ OK, BAD_MAC, TRUNCATED, LENGTH, BAD_TYPE, BAD_VERSION, NO_CONTENT_TYPE = range(7
 APP_DATA = 23
 
 
+def taglen(alg):
+    return 8 if alg.endswith("ccm_8") else 16
+
+
 def _pair(alg):
     if alg.startswith("chacha"):
         return oracle.chacha_seal, oracle.chacha_open
+    if "ccm" in alg:   # AESCCM (aesccm.py), tag 16 or 8
+        t = taglen(alg)
+        return (lambda k, n, p, a: oracle.ccm_seal(k, n, p, a, t),
+                lambda k, n, c, a: oracle.ccm_open(k, n, c, a, t))
     return oracle.gcm_seal, oracle.gcm_open
 
 
@@ -32,7 +40,7 @@ def seal_record(version, alg, key, iv, seq, ctype, data, pad=0):
     data = bytes(data)
     if version == "tls13":
         inner = data + bytes([ctype]) + bytes(pad)
-        n = len(inner) + 16
+        n = len(inner) + taglen(alg)
         hdr = bytes([APP_DATA, 3, 3, n >> 8, n & 0xff])
         return hdr + bytes(seal(key, nonce(version, alg, iv, seq), inner, hdr))
     aad = int(seq).to_bytes(8, "big") + bytes([ctype, 3, 3, len(data) >> 8, len(data) & 0xff])
@@ -57,10 +65,10 @@ def open_record(version, alg, key, iv, seq, wire):
         buf = buf[8:]
     else:
         n = nonce(version, alg, iv, seq)
-    if len(buf) < 16:
+    if len(buf) < taglen(alg):
         return TRUNCATED, 0, b""
     if version == "tls12":
-        plen = len(buf) - 16
+        plen = len(buf) - taglen(alg)
         aad = int(seq).to_bytes(8, "big") + bytes([hdr[0], 3, 3, plen >> 8, plen & 0xff])
     else:
         if hdr[0] != APP_DATA:

@@ -14,14 +14,15 @@ class HostBatch(object):
     16-byte aligned), outputs at ``out_off``, 12-byte nonces, AAD rows."""
 
     def __init__(self, lens, payload_seed=0, align=16, aad_mode="tls13", key_count=1,
-                 iv=None, seq0=0, open_input=None):
+                 iv=None, seq0=0, open_input=None, tag=16):
         rng = np.random.default_rng(payload_seed)
         self.n = n = len(lens)
+        self.tag = tag
         self.lens = np.asarray(lens, dtype=np.uint32)
         step = lambda L: ((L + align - 1) // align) * align if align > 1 else L  # noqa: E731
-        in_sizes = np.array([step(int(L) + (16 if open_input is not None else 0))
+        in_sizes = np.array([step(int(L) + (tag if open_input is not None else 0))
                              for L in self.lens], dtype=np.uint64)
-        out_sizes = np.array([step(int(L) + 16) for L in self.lens], dtype=np.uint64)
+        out_sizes = np.array([step(int(L) + tag) for L in self.lens], dtype=np.uint64)
         self.in_off = np.concatenate([[0], np.cumsum(in_sizes)[:-1]]).astype(np.uint64)
         self.out_off = np.concatenate([[0], np.cumsum(out_sizes)[:-1]]).astype(np.uint64)
         self.in_bytes = int(in_sizes.sum()) + 16
@@ -67,8 +68,46 @@ class HostBatch(object):
     def oracle(self, oracle_mod, alg, keys, op="seal", inp=None, in_off=None, nthreads=8):
         src = self.inp if inp is None else inp
         off = self.in_off if in_off is None else in_off
-        inlen = self.lens + (16 if op == "open" else 0)
+        inlen = self.lens + (self.tag if op == "open" else 0)
         out_off = self.out_off
         return oracle_mod.batch(alg, op, keys, self.nonces, self.aad, self.aad_off, self.aad_len,
                                 src, off, inlen, self.out_bytes, out_off, key_idx=self.key_idx,
                                 nthreads=nthreads)
+
+
+def run_seal_open(torch, tg, oracle_mod, hb, alg, keys, key_obj, tamper=()):
+    """Seal ``hb`` on the GPU, compare with the oracle bit-exact, open the
+    sealed records back (tag bits flipped in ``tamper``) and check status and
+    plaintext (rejected records zeroed)."""
+    T = hb.tag
+    d = hb.to_device(torch)
+    tg.seal_batch(key_obj, hb.batch_kwargs(d))
+    torch.cuda.synchronize()
+    got = d["out"].cpu().numpy()
+    want, _ = hb.oracle(oracle_mod, alg, keys, "seal")
+    for i in range(hb.n):
+        o, L = int(hb.out_off[i]), int(hb.lens[i])
+        assert np.array_equal(got[o:o + L + T], want[o:o + L + T]), ("seal mismatch", i, L)
+    # open the sealed records back (input = ct||tag at out_off)
+    sealed = got.copy()
+    for i in tamper:
+        o, L = int(hb.out_off[i]), int(hb.lens[i])
+        sealed[o + L + (i % T)] ^= 0x20  # flip a tag bit
+    src = torch.from_numpy(sealed).cuda()
+    pt = torch.zeros(hb.in_bytes, dtype=torch.uint8, device="cuda")
+    status = torch.zeros(hb.n, dtype=torch.uint8, device="cuda")
+    b = tg.make_batch(hb.n, src, pt, d["nonces"], aad=d["aad"], lens=d["lens"],
+                      in_off=d["out_off"], out_off=d["in_off"], aad_off=d["aad_off"],
+                      aad_len=d["aad_len"], key_idx=d.get("key_idx"), status=status)
+    tg.open_batch(key_obj, b)
+    torch.cuda.synchronize()
+    st = status.cpu().numpy()
+    back = pt.cpu().numpy()
+    for i in range(hb.n):
+        o, L = int(hb.in_off[i]), int(hb.lens[i])
+        if i in tamper:
+            assert st[i] == 0, i
+            assert not back[o:o + L].any(), "rejected record must be zeroed"
+        else:
+            assert st[i] == 1, i
+            assert np.array_equal(back[o:o + L], hb.inp[o:o + L]), ("open mismatch", i)

@@ -94,37 +94,8 @@ def test_negative(tg):
 # ----------------------------------------------------------- device batches
 
 def _run_seal_open(torch, tg, oracle_mod, hb, alg, keys, key_obj, tamper=()):
-    d = hb.to_device(torch)
-    tg.seal_batch(key_obj, hb.batch_kwargs(d))
-    torch.cuda.synchronize()
-    got = d["out"].cpu().numpy()
-    want, _ = hb.oracle(oracle_mod, alg, keys, "seal")
-    for i in range(hb.n):
-        o, L = int(hb.out_off[i]), int(hb.lens[i])
-        assert np.array_equal(got[o:o + L + 16], want[o:o + L + 16]), ("seal mismatch", i, L)
-    # open the sealed records back (input = ct||tag at out_off)
-    sealed = got.copy()
-    for i in tamper:
-        o, L = int(hb.out_off[i]), int(hb.lens[i])
-        sealed[o + L + (i % 16)] ^= 0x20  # flip a tag bit
-    src = torch.from_numpy(sealed).cuda()
-    pt = torch.zeros(hb.in_bytes, dtype=torch.uint8, device="cuda")
-    status = torch.zeros(hb.n, dtype=torch.uint8, device="cuda")
-    b = tg.make_batch(hb.n, src, pt, d["nonces"], aad=d["aad"], lens=d["lens"],
-                      in_off=d["out_off"], out_off=d["in_off"], aad_off=d["aad_off"],
-                      aad_len=d["aad_len"], key_idx=d.get("key_idx"), status=status)
-    tg.open_batch(key_obj, b)
-    torch.cuda.synchronize()
-    st = status.cpu().numpy()
-    back = pt.cpu().numpy()
-    for i in range(hb.n):
-        o, L = int(hb.in_off[i]), int(hb.lens[i])
-        if i in tamper:
-            assert st[i] == 0, i
-            assert not back[o:o + L].any(), "rejected record must be zeroed"
-        else:
-            assert st[i] == 1, i
-            assert np.array_equal(back[o:o + L], hb.inp[o:o + L]), ("open mismatch", i)
+    from batchpack import run_seal_open
+    run_seal_open(torch, tg, oracle_mod, hb, alg, keys, key_obj, tamper)
 
 
 LEN_MIX = [0, 1, 15, 16, 17, 31, 63, 64, 65, 100, 255, 256, 1000, 1024, 1025, 4096,

@@ -28,25 +28,32 @@ def tg(torch):
 
 
 def _key(tg, alg, key):
-    return tg.HipCHACHA20_POLY1305(bytearray(key)) if alg.startswith("chacha") else \
-        tg.HipAESGCM(bytearray(key))
+    if alg.startswith("chacha"):
+        return tg.HipCHACHA20_POLY1305(bytearray(key))
+    if "ccm" in alg:
+        return tg.HipAESCCM(bytearray(key), tag_length=8 if alg.endswith("_8") else 16)
+    return tg.HipAESGCM(bytearray(key))
+
+
+def _tag(alg):
+    return 8 if alg.endswith("ccm_8") else 16
 
 
 def _hdr(version, alg):
     return 5 + (8 if version == "tls12" and not alg.startswith("chacha") else 0)
 
 
-def _layout(lens, pads, hdr, aligned):
+def _layout(lens, pads, hdr, aligned, tag=16):
     """data offsets (16-aligned, with slack for ctype + padding) and wire
     offsets (payload 16-aligned if ``aligned``, else packed back to back)."""
     data_off, wire_off, d, w = [], [], 0, 0
     for L, p in zip(lens, pads):
         data_off.append(d)
-        d += (L + 1 + p + 16 + 15) // 16 * 16
+        d += (L + 1 + p + tag + 15) // 16 * 16
         if aligned:
             w = (w + hdr + 15) // 16 * 16 - hdr
         wire_off.append(w)
-        w += hdr + L + 1 + p + 16
+        w += hdr + L + 1 + p + tag
     return np.array(data_off, np.int64), np.array(wire_off, np.int64), d + 16, w + 64
 
 
@@ -54,7 +61,7 @@ def _run(torch, tg, version, alg, key, iv, seq0, ctypes_, datas, pads, aligned, 
     n = len(datas)
     lens = [len(x) for x in datas]
     hdr = _hdr(version, alg)
-    data_off, wire_off, dsz, wsz = _layout(lens, pads, hdr, aligned)
+    data_off, wire_off, dsz, wsz = _layout(lens, pads, hdr, aligned, _tag(alg))
     host = np.zeros(dsz, np.uint8)
     for o, x in zip(data_off, datas):
         host[o:o + len(x)] = np.frombuffer(bytes(x), np.uint8)
@@ -110,7 +117,8 @@ def test_reference_wire_bytes(torch, tg, ci, aligned):
 
 @pytest.mark.parametrize("version,alg,klen,ivlen", [
     ("tls13", "aes128gcm", 16, 12), ("tls13", "chacha20-poly1305", 32, 12),
-    ("tls12", "aes256gcm", 32, 4), ("tls12", "chacha20-poly1305", 32, 12)])
+    ("tls12", "aes256gcm", 32, 4), ("tls12", "chacha20-poly1305", 32, 12),
+    ("tls13", "aes128ccm_8", 16, 12), ("tls12", "aes256ccm", 32, 4)])
 def test_random_batch_vs_oracle_and_errors(torch, tg, version, alg, klen, ivlen):
     from oracle import records as R
     rng = np.random.default_rng(klen + ivlen)

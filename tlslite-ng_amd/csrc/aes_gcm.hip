@@ -22,45 +22,10 @@
 #include <cstdlib>
 #include <type_traits>
 
-#include "common.h"
+#include "aes_round.h"
 
 namespace tg {
 namespace {
-
-// ---- Te0 generated at compile time from GF(2^8) exp/log tables ----------
-struct TeTable {
-    uint32_t te0[256];
-};
-
-constexpr uint8_t xtime(uint8_t a) { return (uint8_t)((a << 1) ^ ((a & 0x80) ? 0x1b : 0)); }
-
-constexpr TeTable make_te() {
-    uint8_t exp[256] = {};
-    uint8_t log[256] = {};
-    uint8_t x = 1;
-    for (int i = 0; i < 255; ++i) {
-        exp[i] = x;
-        log[x] = (uint8_t)i;
-        x = (uint8_t)(x ^ xtime(x));  // times generator 3
-    }
-    TeTable t = {};
-    for (int v = 0; v < 256; ++v) {
-        uint8_t inv = v ? exp[(255 - log[v]) % 255] : 0;
-        uint8_t s = inv, r = inv;
-        for (int k = 0; k < 4; ++k) {
-            r = (uint8_t)((r << 1) | (r >> 7));
-            s = (uint8_t)(s ^ r);
-        }
-        s = (uint8_t)(s ^ 0x63);
-        uint8_t s2 = xtime(s);
-        uint8_t s3 = (uint8_t)(s2 ^ s);
-        // column contribution of a row-0 byte: rows (2s, s, s, 3s), LE word
-        t.te0[v] = (uint32_t)s2 | ((uint32_t)s << 8) | ((uint32_t)s << 16) | ((uint32_t)s3 << 24);
-    }
-    return t;
-}
-
-__constant__ TeTable c_te = make_te();
 
 // LDS map (one workgroup per CU, no static LDS so the dynamic block is at 0):
 //   [0, 64 KiB)        GHASH tables, entry (j, b) = M_j[b] at j * 4096 + b * 16
@@ -74,126 +39,6 @@ constexpr uint32_t kTeBase = 65536;
 constexpr size_t kGcmLds = 2 * 65536;
 
 extern __shared__ __attribute__((aligned(16))) uint4 g_lds[];
-
-#if defined(__HIP_DEVICE_COMPILE__)
-typedef const __attribute__((address_space(3))) uint32_t* lds_u32_ptr;
-typedef const __attribute__((address_space(3))) uint4* lds_u128_ptr;
-__device__ __forceinline__ uint32_t lds_u32(uint32_t addr) { return *(lds_u32_ptr)(uintptr_t)addr; }
-__device__ __forceinline__ uint4 lds_u128(uint32_t addr) { return *(lds_u128_ptr)(uintptr_t)addr; }
-__device__ __forceinline__ uint4 lds_u128_v(uint32_t addr) {
-    const volatile __attribute__((address_space(3))) uint4* p =
-        (const volatile __attribute__((address_space(3))) uint4*)(uintptr_t)addr;
-    uint4 v;
-    v.x = p->x; v.y = p->y; v.z = p->z; v.w = p->w;
-    return v;
-}
-__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
-    return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
-}
-__device__ __forceinline__ uint32_t and_or(uint32_t a, uint32_t b, uint32_t c) {  // (a & b) | c
-    return __builtin_amdgcn_bitop3_b32(a, b, c, 0xEA);
-}
-#else
-__device__ __forceinline__ uint32_t lds_u32(uint32_t) { return 0; }
-__device__ __forceinline__ uint4 lds_u128(uint32_t) { return uint4(); }
-__device__ __forceinline__ uint4 lds_u128_v(uint32_t) { return uint4(); }
-__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) { return a ^ b ^ c; }
-__device__ __forceinline__ uint32_t and_or(uint32_t a, uint32_t b, uint32_t c) { return (a & b) | c; }
-#endif
-
-__device__ __forceinline__ uint4 xor4_3(uint4 a, uint4 b, uint4 c) {
-    return make_uint4(xor3(a.x, b.x, c.x), xor3(a.y, b.y, c.y), xor3(a.z, b.z, c.z),
-                      xor3(a.w, b.w, c.w));
-}
-
-// Byte address of row (byte K of x) for this lane; lane4 = 0x10000 | (lane%32)*4.
-template <int K>
-__device__ __forceinline__ uint32_t te_addr(uint32_t x, uint32_t lane4) {
-    if (K == 1) return and_or(x, 0xff00u, lane4);   // one full-rate bitop3
-    return __builtin_amdgcn_perm(x, lane4, 0x0c020000u | ((4u + K) << 8));
-}
-template <int K>
-__device__ __forceinline__ uint32_t T0(uint32_t x, uint32_t lane4) { return lds_u32(te_addr<K>(x, lane4)); }
-template <int K>
-__device__ __forceinline__ uint32_t T2(uint32_t x, uint32_t lane4) { return lds_u32(te_addr<K>(x, lane4) + 128); }
-
-// One T-table round column: rows from s_a byte 0, s_b byte 1, s_c byte 2, s_d byte 3.
-__device__ __forceinline__ uint32_t col(uint32_t sa, uint32_t sb, uint32_t sc, uint32_t sd,
-                                        uint32_t rk, uint32_t lane4) {
-    return xor3(T0<0>(sa, lane4), T2<2>(sc, lane4), rk) ^
-           rotl32(T0<1>(sb, lane4) ^ T2<3>(sd, lane4), 8);
-}
-
-// Final round column: S(x) is byte 1 of Te0[x].
-__device__ __forceinline__ uint32_t col_last(uint32_t sa, uint32_t sb, uint32_t sc, uint32_t sd,
-                                             uint32_t rk, uint32_t lane4) {
-    const uint32_t lo = __builtin_amdgcn_perm(T0<1>(sb, lane4), T0<0>(sa, lane4), 0x0c0c0501u);
-    const uint32_t hi = __builtin_amdgcn_perm(T0<3>(sd, lane4), T0<2>(sc, lane4), 0x05010c0cu);
-    return xor3(lo, hi, rk);
-}
-
-// Round-key providers: get(r) = the four words of round key r.
-template <int NR>
-struct RkRegs {  // single key per launch: wave-uniform, lives in SGPRs
-    uint32_t w[4 * (NR + 1)];
-    __device__ __forceinline__ uint4 get(int r) const {
-        return make_uint4(w[4 * r], w[4 * r + 1], w[4 * r + 2], w[4 * r + 3]);
-    }
-};
-struct RkLds {  // key table: this lane's schedule staged in an LDS row
-    uint32_t base;
-    // volatile: re-read per round instead of being hoisted into 60 VGPRs
-    __device__ __forceinline__ uint4 get(int r) const { return lds_u128_v(base + 16 * r); }
-};
-
-// Per-record round-1 constants for counter mode: after AddRoundKey the state
-// words s0..s2 (nonce ^ rk0) are the same for every block of the record, so
-// each round-1 column is a constant K_c XOR the one term that reads s3.
-struct CtrCache {
-    uint32_t k0, k1, k2, k3;
-};
-
-template <int NR, class RK>
-__device__ __forceinline__ CtrCache ctr_cache(uint32_t lane4, const RK& rkp, uint4 nv) {
-    const uint4 k0 = rkp.get(0), k1 = rkp.get(1);
-    const uint32_t s0 = nv.x ^ k0.x, s1 = nv.y ^ k0.y, s2 = nv.z ^ k0.z;
-    const uint32_t rk[8] = {k0.x, k0.y, k0.z, k0.w, k1.x, k1.y, k1.z, k1.w};
-    CtrCache c;
-    // column 0: a=s0.b0 b=s1.b1 c=s2.b2 d=s3.b3(varies)
-    c.k0 = T0<0>(s0, lane4) ^ T2<2>(s2, lane4) ^ rotl32(T0<1>(s1, lane4), 8) ^ rk[4];
-    // column 1: a=s1.b0 b=s2.b1 c=s3.b2(varies) d=s0.b3
-    c.k1 = T0<0>(s1, lane4) ^ rotl32(T0<1>(s2, lane4) ^ T2<3>(s0, lane4), 8) ^ rk[5];
-    // column 2: a=s2.b0 b=s3.b1(varies) c=s0.b2 d=s1.b3
-    c.k2 = T0<0>(s2, lane4) ^ T2<2>(s0, lane4) ^ rotl32(T2<3>(s1, lane4), 8) ^ rk[6];
-    // column 3: a=s3.b0(varies) b=s0.b1 c=s1.b2 d=s2.b3
-    c.k3 = T2<2>(s1, lane4) ^ rotl32(T0<1>(s0, lane4) ^ T2<3>(s2, lane4), 8) ^ rk[7];
-    return c;
-}
-
-// E_K(nonce || be32(ctr)) using the round-1 cache.
-template <int NR, class RK>
-__device__ __forceinline__ uint4 aes_ctr(uint32_t lane4, const RK& rkp, const CtrCache& cc,
-                                         uint32_t ctr) {
-    uint32_t s3 = bswap32(ctr) ^ rkp.get(0).w;
-    uint32_t s0 = cc.k0 ^ rotl32(T2<3>(s3, lane4), 8);
-    uint32_t s1 = cc.k1 ^ T2<2>(s3, lane4);
-    uint32_t s2 = cc.k2 ^ rotl32(T0<1>(s3, lane4), 8);
-    uint32_t t3 = cc.k3 ^ T0<0>(s3, lane4);
-    uint32_t t0, t1, t2;
-    s3 = t3;
-#pragma unroll
-    for (int r = 2; r < NR; ++r) {
-        const uint4 k = rkp.get(r);
-        t0 = col(s0, s1, s2, s3, k.x, lane4);
-        t1 = col(s1, s2, s3, s0, k.y, lane4);
-        t2 = col(s2, s3, s0, s1, k.z, lane4);
-        t3 = col(s3, s0, s1, s2, k.w, lane4);
-        s0 = t0; s1 = t1; s2 = t2; s3 = t3;
-    }
-    const uint4 k = rkp.get(NR);
-    return make_uint4(col_last(s0, s1, s2, s3, k.x, lane4), col_last(s1, s2, s3, s0, k.y, lane4),
-                      col_last(s2, s3, s0, s1, k.z, lane4), col_last(s3, s0, s1, s2, k.w, lane4));
-}
 
 // y * H with the sixteen 8-bit tables: X * H = XOR_j M_j[byte j of X]; byte j
 // of the block is byte j%4 of word j/4.  Entry (j, b) sits at j * 4096 + b * 16
@@ -460,13 +305,7 @@ __global__ __launch_bounds__(THREADS) void gcm_kernel(const GcmKeyDev* __restric
     // stage the GHASH tables (ROT: row layout b * 16 + j) and the Te0/Te2 copies
     for (int e = threadIdx.x; e < kGhashEntries; e += blockDim.x)
         lds[ROT ? (e & 255) * 16 + (e >> 8) : e] = key->ghash[e];
-    {
-        uint32_t* te = reinterpret_cast<uint32_t*>(lds) + kTeBase / 4;
-        for (int e = threadIdx.x; e < 256 * 64; e += blockDim.x) {
-            const uint32_t v = c_te.te0[e >> 6];
-            te[e] = (e & 32) ? rotl32(v, 16) : v;
-        }
-    }
+    stage_te(reinterpret_cast<uint32_t*>(lds) + kTeBase / 4);
     RkRegs<NR> rk;
 #pragma unroll
     for (int k = 0; k < 4 * (NR + 1); ++k) rk.w[k] = key->rk[k];
@@ -491,13 +330,7 @@ template <int NR, bool OPEN, int G>
 __global__ __launch_bounds__(kMkThreads, 4) void gcm_table_kernel(const GcmTableKey* __restrict__ keys,
                                                               tg_batch b) {
     uint4* lds = g_lds;
-    {
-        uint32_t* te = reinterpret_cast<uint32_t*>(lds);  // Te0/Te2 copies at LDS 0
-        for (int e = threadIdx.x; e < 256 * 64; e += blockDim.x) {
-            const uint32_t v = c_te.te0[e >> 6];
-            te[e] = (e & 32) ? rotl32(v, 16) : v;
-        }
-    }
+    stage_te(reinterpret_cast<uint32_t*>(lds));  // Te0/Te2 copies at LDS 0
     __syncthreads();
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= b.n) return;

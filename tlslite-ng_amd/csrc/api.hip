@@ -160,8 +160,10 @@ struct tg_key {
     size_t nkeys;
     int device;
     int rounds;
+    int taglen;             // 16, or 8 for AES-CCM_8
     hipStream_t stream;
-    void* dev_key;          // GcmKeyDev (AES) or ChachaKeyDev[nkeys]
+    void* dev_key;          // GcmKeyDev / GcmTableKey[nkeys] (AES-GCM),
+                            // AesKeyDev[nkeys] (AES-CCM), ChachaKeyDev[nkeys]
     // staging for the per-record drop-in path
     uint8_t* h_stage;
     uint8_t* d_stage;
@@ -192,7 +194,18 @@ int ensure_stage(tg_key* k, size_t bytes) {
     return TG_OK;
 }
 
+bool is_ccm(int alg) { return alg == TG_AES_CCM || alg == TG_AES_CCM_8; }
+
+size_t dev_key_bytes(const tg_key* k) {
+    if (k->alg == TG_CHACHA20_POLY1305) return sizeof(tg::ChachaKeyDev) * k->nkeys;
+    if (is_ccm(k->alg)) return sizeof(tg::AesKeyDev) * k->nkeys;
+    return k->nkeys > 1 ? sizeof(tg::GcmTableKey) * k->nkeys : sizeof(tg::GcmKeyDev);
+}
+
 int launch(tg_key* k, const tg_batch& b, bool open, hipStream_t s) {
+    if (is_ccm(k->alg))
+        return tg_launch_ccm(static_cast<const tg::AesKeyDev*>(k->dev_key), k->nkeys > 1,
+                             k->rounds, k->taglen, b, open, s);
     if (k->alg == TG_AES_GCM && k->nkeys > 1)
         return tg_launch_gcm_table(static_cast<const tg::GcmTableKey*>(k->dev_key), k->rounds, b,
                                    open, s);
@@ -210,13 +223,15 @@ int single(tg_key* k, const uint8_t* nonce, size_t noncelen, const uint8_t* aad,
     if (k->nkeys != 1) return fail(TG_EINVAL, "per-record calls need a single-key handle");
     if (noncelen != 12) return fail(TG_ENONCE, "Bad nonce length");
     if ((aadlen && !aad) || (inlen && !in)) return fail(TG_EINVAL, "null buffer");
-    if (open && inlen < 16) {   // aesgcm.py:135-136, chacha20_poly1305.py:76-77
+    const size_t T = (size_t)k->taglen;
+    if (open && inlen < T) {   // aesgcm.py:135-136, chacha20_poly1305.py:76-77, aesccm.py:120-123
         return 0;
     }
-    const size_t len = open ? inlen - 16 : inlen;
+    const size_t len = open ? inlen - T : inlen;
     if (len > 0xffffffffull || aadlen > 0xffffffffull) return fail(TG_EINVAL, "record too long");
+    if (is_ccm(k->alg) && len >= (1ull << 28) - 32) return fail(TG_EINVAL, "CCM record too long");
     const size_t o_aad = 16, o_in = align16(o_aad + aadlen), o_out = align16(o_in + inlen);
-    const size_t outlen = open ? len : len + 16;
+    const size_t outlen = open ? len : len + T;
     const size_t o_st = align16(o_out + outlen), total = o_st + 16;
     int rc = select_device(k);
     if (rc) return rc;
@@ -310,8 +325,9 @@ int records(tg_key* k, const tg_records* r, void* stream, bool seal) {
     ScratchAlloc alloc;
     tg::RecScratch s;
     if ((rc = records_scratch(r->n, st, alloc, s))) return rc;
-    const bool aes = k->alg == TG_AES_GCM;
-    if ((rc = tg_launch_records_prep(*r, seal, aes, s, st))) return fail(rc, "framing launch failed");
+    const bool aes = k->alg != TG_CHACHA20_POLY1305;   // "aes" in name (recordlayer.py:561, :783)
+    if ((rc = tg_launch_records_prep(*r, seal, aes, k->taglen, s, st)))
+        return fail(rc, "framing launch failed");
     tg_batch b;
     memset(&b, 0, sizeof(b));
     b.n = r->n;
@@ -365,8 +381,9 @@ int tg_init(int device) {
 int tg_key_create(int alg, const uint8_t* keys, size_t keylen, size_t nkeys, tg_key** out) {
     if (!out || !keys || nkeys == 0) return fail(TG_EINVAL, "null argument");
     *out = nullptr;
-    if (alg == TG_AES_GCM) {
-        if (keylen != 16 && keylen != 32) return fail(TG_EKEYLEN, "AES-GCM key must be 16 or 32 bytes");
+    if (alg == TG_AES_GCM || is_ccm(alg)) {
+        // AssertionError in AESGCM.__init__ (aesgcm.py:37-38) and AESCCM.__init__ (aesccm.py:22-30)
+        if (keylen != 16 && keylen != 32) return fail(TG_EKEYLEN, "AES key must be 16 or 32 bytes");
     } else if (alg == TG_CHACHA20_POLY1305) {
         if (keylen != 32) return fail(TG_EKEYLEN, "Key must be 256 bit long");
     } else {
@@ -379,6 +396,7 @@ int tg_key_create(int alg, const uint8_t* keys, size_t keylen, size_t nkeys, tg_
     k->alg = alg;
     k->keylen = keylen;
     k->nkeys = nkeys;
+    k->taglen = alg == TG_AES_CCM_8 ? 8 : 16;
     k->device = dev;
     int rc = TG_OK;
     hipError_t e = hipStreamCreateWithFlags(&k->stream, hipStreamNonBlocking);
@@ -386,7 +404,27 @@ int tg_key_create(int alg, const uint8_t* keys, size_t keylen, size_t nkeys, tg_
         delete k;
         return fail(TG_EHIP, "hipStreamCreate: %s", hipGetErrorString(e));
     }
-    if (alg == TG_AES_GCM && nkeys > 1) {
+    if (is_ccm(alg)) {
+        tg::AesKeyDev* hk = new (std::nothrow) tg::AesKeyDev[nkeys];
+        if (!hk) rc = fail(TG_ENOMEM, "out of host memory");
+        if (!rc) {
+            const HostAes& aes = host_aes();
+            for (size_t i = 0; i < nkeys; ++i) {
+                uint8_t rk[240] = {0};
+                const int nr = aes.expand(keys + keylen * i, keylen, rk);
+                memset(&hk[i], 0, sizeof(hk[i]));
+                for (int w = 0; w < 4 * (nr + 1); ++w) hk[i].rk[w] = le32(rk + 4 * w);
+                k->rounds = nr;
+                memset(rk, 0, sizeof(rk));
+            }
+            const size_t bytes = sizeof(tg::AesKeyDev) * nkeys;
+            e = hipMalloc(&k->dev_key, bytes);
+            if (e == hipSuccess) e = hipMemcpy(k->dev_key, hk, bytes, hipMemcpyHostToDevice);
+            if (e != hipSuccess) rc = fail(TG_EHIP, "key upload: %s", hipGetErrorString(e));
+            memset(hk, 0, sizeof(tg::AesKeyDev) * nkeys);
+            delete[] hk;
+        }
+    } else if (alg == TG_AES_GCM && nkeys > 1) {
         tg::GcmTableKey* hk = new (std::nothrow) tg::GcmTableKey[nkeys];
         if (!hk) rc = fail(TG_ENOMEM, "out of host memory");
         if (!rc) {
@@ -466,10 +504,7 @@ int tg_key_destroy(tg_key* k) {
     if (k->stream) (void)hipStreamSynchronize(k->stream);
     if (k->dev_key) {
         // scrub key material before release
-        size_t bytes = k->alg != TG_AES_GCM ? sizeof(tg::ChachaKeyDev) * k->nkeys
-                       : k->nkeys > 1   ? sizeof(tg::GcmTableKey) * k->nkeys
-                                        : sizeof(tg::GcmKeyDev);
-        (void)hipMemset(k->dev_key, 0, bytes);
+        (void)hipMemset(k->dev_key, 0, dev_key_bytes(k));
         (void)hipFree(k->dev_key);
     }
     if (k->h_stage) (void)hipHostFree(k->h_stage);
@@ -488,6 +523,11 @@ int tg_key_info(const tg_key* k, int* alg, size_t* keylen, size_t* nkeys) {
     return TG_OK;
 }
 
+int tg_key_taglen(const tg_key* k) {
+    if (!k) return fail(TG_EINVAL, "null key");
+    return k->taglen;
+}
+
 int tg_seal(tg_key* k, const uint8_t* nonce, size_t noncelen, const uint8_t* aad, size_t aadlen,
             const uint8_t* pt, size_t len, uint8_t* out) {
     if (!out) return fail(TG_EINVAL, "null output");
@@ -496,7 +536,7 @@ int tg_seal(tg_key* k, const uint8_t* nonce, size_t noncelen, const uint8_t* aad
 
 int tg_open(tg_key* k, const uint8_t* nonce, size_t noncelen, const uint8_t* aad, size_t aadlen,
             const uint8_t* in, size_t inlen, uint8_t* pt) {
-    if (!pt && inlen > 16) return fail(TG_EINVAL, "null output");
+    if (!pt && k && inlen > (size_t)k->taglen) return fail(TG_EINVAL, "null output");
     return single(k, nonce, noncelen, aad, aadlen, in, inlen, pt, true);
 }
 

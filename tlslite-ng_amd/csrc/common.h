@@ -31,6 +31,12 @@ struct GcmTableKey {
     uint32_t hn[4];
 };
 
+// One AES key (AES-CCM): the round keys; a key table is an array of these.
+struct AesKeyDev {
+    uint32_t rk[60];
+    uint32_t pad[4];
+};
+
 struct ChachaKeyDev {
     uint32_t k[8];         // key as LE words (chacha.py:101, _bytearray_to_words)
 };
@@ -126,9 +132,11 @@ int tg_launch_gcm(const tg::GcmKeyDev* key, int rounds, const tg_batch& b, bool 
                   hipStream_t s);
 int tg_launch_gcm_table(const tg::GcmTableKey* keys, int rounds, const tg_batch& b, bool open,
                         hipStream_t s);
+int tg_launch_ccm(const tg::AesKeyDev* keys, bool table, int rounds, int taglen,
+                  const tg_batch& b, bool open, hipStream_t s);
 int tg_launch_chacha(const tg::ChachaKeyDev* keys, const tg_batch& b, bool open, hipStream_t s);
-int tg_launch_records_prep(const tg_records& r, bool seal, bool aes, const tg::RecScratch& s,
-                           hipStream_t st);
+int tg_launch_records_prep(const tg_records& r, bool seal, bool aes, int taglen,
+                           const tg::RecScratch& s, hipStream_t st);
 int tg_launch_records_finish(const tg_records& r, const tg::RecScratch& s, hipStream_t st);
 int tg_launch_nonces(int mode, const uint8_t* iv_host, uint64_t seq0, uint64_t n, uint8_t* out,
                      hipStream_t s);

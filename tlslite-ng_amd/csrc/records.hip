@@ -46,7 +46,7 @@ __device__ __forceinline__ void rec_nonce(const tg_records& r, bool xor_form, ui
     }
 }
 
-__global__ void seal_prep(tg_records r, bool aes, RecScratch s) {
+__global__ void seal_prep(tg_records r, bool aes, uint32_t taglen, RecScratch s) {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= r.n) return;
     const bool tls13 = r.version == TG_TLS13;
@@ -62,7 +62,7 @@ __global__ void seal_prep(tg_records r, bool aes, RecScratch s) {
         inner = L + 1 + pad;
     }
     const uint32_t explicit_len = (!tls13 && aes) ? 8 : 0;
-    const uint32_t body = explicit_len + inner + 16;
+    const uint32_t body = explicit_len + inner + taglen;
     uint8_t* w = r.wire + r.wire_off[i];
     w[0] = tls13 ? kAppData : ct;   // TLS 1.3 hides the type (:614)
     w[1] = 3;
@@ -74,7 +74,7 @@ __global__ void seal_prep(tg_records r, bool aes, RecScratch s) {
     s.len[i] = inner;
     rec_nonce(r, tls13 || (!aes && r.fixed_iv_len == 12), seq, s.nonce + 12 * i);
     uint8_t* a = s.aad + 16 * i;
-    if (tls13) {  // AAD = the record header (:546-552)
+    if (tls13) {  // AAD = the record header, length = inner + tag (:546-552)
         for (int k = 0; k < 5; ++k) a[k] = w[k];
         s.aad_len[i] = 5;
     } else {      // seq || type || version || length (:540-545)
@@ -87,7 +87,7 @@ __global__ void seal_prep(tg_records r, bool aes, RecScratch s) {
     }
 }
 
-__global__ void open_prep(tg_records r, bool aes, RecScratch s) {
+__global__ void open_prep(tg_records r, bool aes, uint32_t taglen, RecScratch s) {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= r.n) return;
     const bool tls13 = r.version == TG_TLS13;
@@ -98,7 +98,7 @@ __global__ void open_prep(tg_records r, bool aes, RecScratch s) {
     uint8_t st = TG_REC_OK;
     const uint32_t explicit_len = (!tls13 && aes) ? 8 : 0;
     if (wl < 5 || explicit_len > buf_len) st = TG_REC_TRUNCATED;           // :787-789
-    else if (buf_len - explicit_len < 16) st = TG_REC_TRUNCATED;           // :797-799
+    else if (buf_len - explicit_len < taglen) st = TG_REC_TRUNCATED;       // :797-799
     const uint8_t type = wl >= 1 ? w[0] : 0;
     if (st == TG_REC_OK && tls13) {
         const uint32_t ver = ((uint32_t)w[1] << 8) | w[2];
@@ -108,7 +108,7 @@ __global__ void open_prep(tg_records r, bool aes, RecScratch s) {
         else if (hlen != buf_len) st = TG_REC_LENGTH;                      // :816-817
     }
     s.st[i] = st;
-    const uint32_t ct_len = st == TG_REC_OK ? buf_len - explicit_len - 16 : 0;
+    const uint32_t ct_len = st == TG_REC_OK ? buf_len - explicit_len - taglen : 0;
     s.len[i] = ct_len;
     // invalid records run the AEAD over an empty message with a dummy tag
     s.in_abs[i] = st == TG_REC_OK ? (uint64_t)(uintptr_t)(w + 5 + explicit_len)
@@ -168,15 +168,15 @@ __global__ void open_finish(tg_records r, RecScratch s) {
 }  // namespace
 }  // namespace tg
 
-int tg_launch_records_prep(const tg_records& r, bool seal, bool aes, const tg::RecScratch& s,
-                           hipStream_t st) {
+int tg_launch_records_prep(const tg_records& r, bool seal, bool aes, int taglen,
+                           const tg::RecScratch& s, hipStream_t st) {
     const uint64_t blocks = (r.n + tg::kRecThreads - 1) / tg::kRecThreads;
     if (seal)
         hipLaunchKernelGGL(tg::seal_prep, dim3((unsigned)blocks), dim3(tg::kRecThreads), 0, st, r,
-                           aes, s);
+                           aes, (uint32_t)taglen, s);
     else
         hipLaunchKernelGGL(tg::open_prep, dim3((unsigned)blocks), dim3(tg::kRecThreads), 0, st, r,
-                           aes, s);
+                           aes, (uint32_t)taglen, s);
     return hipGetLastError() == hipSuccess ? TG_OK : TG_EHIP;
 }
 

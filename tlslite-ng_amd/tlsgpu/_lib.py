@@ -20,10 +20,12 @@ TG_ENODEV = -19
 
 TG_AES_GCM = 0
 TG_CHACHA20_POLY1305 = 1
+TG_AES_CCM = 2
+TG_AES_CCM_8 = 3
 
 # Every function include/tlsgpu.h declares (checked by tests/test_abi.py).
 EXPORTS = ("tg_version", "tg_last_error", "tg_device_count", "tg_init", "tg_key_create",
-           "tg_key_destroy", "tg_key_info", "tg_seal", "tg_open", "tg_seal_batch",
+           "tg_key_destroy", "tg_key_info", "tg_key_taglen", "tg_seal", "tg_open", "tg_seal_batch",
            "tg_open_batch", "tg_make_nonces", "tg_malloc", "tg_free", "tg_memcpy_h2d",
            "tg_memcpy_d2h", "tg_stream_sync", "tg_seal_records", "tg_open_records")
 
@@ -107,6 +109,7 @@ def load():
     l.tg_key_destroy.argtypes = [p]
     l.tg_key_info.argtypes = [p, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(sz),
                               ctypes.POINTER(sz)]
+    l.tg_key_taglen.argtypes = [p]
     l.tg_seal.argtypes = [p, p, sz, p, sz, p, sz, p]
     l.tg_open.argtypes = [p, p, sz, p, sz, p, sz, p]
     l.tg_seal_batch.argtypes = [p, ctypes.POINTER(TgBatch), p]

@@ -1,12 +1,13 @@
 """AEAD objects with the reference's object contract, backed by libtlsgpu.
 
-``HipAESGCM`` and ``HipCHACHA20_POLY1305`` expose exactly what
+``HipAESGCM``, ``HipAESCCM`` and ``HipCHACHA20_POLY1305`` expose exactly what
 tlslite/recordlayer.py reads from an AEAD:
 ``isBlockCipher``, ``isAEAD``, ``name``, ``implementation``, ``nonceLength``,
 ``tagLength``, ``key``, ``seal(nonce, plaintext, data) -> ct||tag`` and
 ``open(nonce, ciphertext, data) -> plaintext or None``, with the error
 conventions of tlslite/utils/aesgcm.py:27-154 (AssertionError on a bad key
-length, ValueError on a bad nonce length) and
+length, ValueError on a bad nonce length), tlslite/utils/aesccm.py:11-149
+(the same, with an 8- or 16-byte tag) and
 tlslite/utils/chacha20_poly1305.py:19-94 (ValueError on either).  Objects are
 stateless per call and survive ``copy.copy`` (recordlayer.py:262, :913):
 copies share one refcounted device key.
@@ -57,7 +58,7 @@ class _HipAEAD(object):
             raise ValueError(self._nonce_msg)
         pt = _as_bytes(plaintext)
         aad = _as_bytes(data)
-        out = ctypes.create_string_buffer(len(pt) + 16)
+        out = ctypes.create_string_buffer(len(pt) + self.tagLength)
         _lib.check(self._dkey._lib.tg_seal(self._dkey.handle, _as_bytes(nonce), 12, aad,
                                            len(aad), pt, len(pt), out))
         return bytearray(out.raw)
@@ -66,16 +67,17 @@ class _HipAEAD(object):
         """Verify then decrypt; returns the plaintext or None."""
         if len(nonce) != 12:
             raise ValueError(self._nonce_msg)
-        if len(ciphertext) < 16:
+        T = self.tagLength
+        if len(ciphertext) < T:
             return None
         ct = _as_bytes(ciphertext)
         aad = _as_bytes(data)
-        out = ctypes.create_string_buffer(max(len(ct) - 16, 1))
+        out = ctypes.create_string_buffer(max(len(ct) - T, 1))
         rc = _lib.check(self._dkey._lib.tg_open(self._dkey.handle, _as_bytes(nonce), 12, aad,
                                                 len(aad), ct, len(ct), out))
         if rc != 1:
             return None
-        return bytearray(out.raw[:len(ct) - 16])
+        return bytearray(out.raw[:len(ct) - T])
 
 
 class HipAESGCM(_HipAEAD):
@@ -91,6 +93,27 @@ class HipAESGCM(_HipAEAD):
         else:
             raise AssertionError()
         super(HipAESGCM, self).__init__(key, implementation)
+
+
+class HipAESCCM(_HipAEAD):
+    """Drop-in for ``AESCCM`` (tlslite/utils/aesccm.py:11): ``tag_length`` 16
+    (``aes128ccm`` / ``aes256ccm``) or 8 (``aes128ccm_8`` / ``aes256ccm_8``)."""
+    _nonce_msg = "Bad nonce length"
+
+    def __init__(self, key, implementation="hip", tag_length=16):
+        # aesccm.py:22-30: any other key / tag combination is an AssertionError
+        if len(key) == 16 and tag_length == 8:
+            self.name = "aes128ccm_8"
+        elif len(key) == 16 and tag_length == 16:
+            self.name = "aes128ccm"
+        elif len(key) == 32 and tag_length == 8:
+            self.name = "aes256ccm_8"
+        else:
+            assert len(key) == 32 and tag_length == 16
+            self.name = "aes256ccm"
+        self.tagLength = tag_length
+        self._alg = _lib.TG_AES_CCM if tag_length == 16 else _lib.TG_AES_CCM_8
+        super(HipAESCCM, self).__init__(key, implementation)
 
 
 class HipCHACHA20_POLY1305(_HipAEAD):

@@ -55,9 +55,12 @@ class KeyTable(object):
         keys = [bytes(k) for k in keys]
         if not keys or len(set(len(k) for k in keys)) != 1:
             raise ValueError("keys must be a non-empty list of equal-length keys")
-        code = {"aesgcm": _lib.TG_AES_GCM, "chacha20-poly1305": _lib.TG_CHACHA20_POLY1305}[alg]
+        code = {"aesgcm": _lib.TG_AES_GCM, "aesccm": _lib.TG_AES_CCM,
+                "aesccm_8": _lib.TG_AES_CCM_8,
+                "chacha20-poly1305": _lib.TG_CHACHA20_POLY1305}[alg]
         self.alg = alg
         self.nkeys = len(keys)
+        self.tagLength = 8 if alg == "aesccm_8" else 16
         self._dkey = _DeviceKey(code, b"".join(keys), len(keys))
 
 

@@ -5,7 +5,7 @@ of consecutive records of one connection direction (record i has sequence
 number ``seq0 + i``):
 
 * seal: fragment + content type (+ TLS 1.3 zero padding) -> wire record
-  ``header || [TLS 1.2 AES-GCM explicit nonce] || ciphertext || tag``
+  ``header || [TLS 1.2 AES-GCM/CCM explicit nonce] || ciphertext || tag``
   (``sendRecord`` :606-617, ``_encryptThenSeal`` :536-565, ``_getNonce``
   :522-534);
 * open: wire record -> plaintext, content type and a per-record status
