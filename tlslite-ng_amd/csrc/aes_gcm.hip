@@ -36,7 +36,7 @@ namespace {
 //     Te0[a] ^ rotl8(Te0[b]) ^ rotl16(Te0[c]) ^ rotl24(Te0[d])
 //       = Te0[a] ^ Te2[c] ^ rotl8(Te0[b] ^ Te2[d]).
 constexpr uint32_t kTeBase = 65536;
-constexpr size_t kGcmLds = 2 * 65536;
+constexpr size_t kGcmLds = 2 * 65536 + 256;   // + the GhashTablesRotLds offsets
 
 extern __shared__ __attribute__((aligned(16))) uint4 g_lds[];
 
@@ -109,6 +109,43 @@ struct GhashTablesRot {
             // byte 1 <- v[t/4] byte t%4 (the row b), byte 0 <- jt[t/4] byte t%4
             const uint32_t sel = 0x0c0c0000u | ((4u + (t & 3)) << 8) | (uint32_t)(t & 3);
             e[t] = lds_u128(__builtin_amdgcn_perm(v[t >> 2], jt[t >> 2], sel));
+        }
+        uint4 z = xor4_3(e[0], e[1], e[2]);
+        z = xor4_3(z, e[3], e[4]);
+        z = xor4_3(z, e[5], e[6]);
+        z = xor4_3(z, e[7], e[8]);
+        z = xor4_3(z, e[9], e[10]);
+        z = xor4_3(z, e[11], e[12]);
+        z = xor4_3(z, e[13], e[14]);
+        return xor4(z, e[15]);
+    }
+    __device__ __forceinline__ uint4 update(uint4 y, uint4 blk) const { return mul(xor4(y, blk)); }
+    __device__ __forceinline__ uint4 finish(uint4 y) const { return y; }
+};
+
+// GhashTablesRot without persistent per-lane state: the rotation amounts are
+// bits of lane4 (the AES lookup register, bits 2..5 = lane % 16) and the four
+// table-offset words come from a 16-row LDS table (one conflict-free
+// ds_read_b128 per multiply), which frees the 7 VGPRs GhashTablesRot holds.
+constexpr uint32_t kJtBase = 2 * 65536;
+struct GhashTablesRotLds {
+    uint32_t lane4;
+    __device__ __forceinline__ uint4 mul(uint4 y) const {
+        const uint4 jt = lds_u128(kJtBase + ((lane4 & 0x3cu) << 2));
+        uint32_t u0 = y.x, u1 = y.y, u2 = y.z, u3 = y.w;
+        if (lane4 & 0x20u) { uint32_t t = u0; u0 = u2; u2 = t; t = u1; u1 = u3; u3 = t; }
+        if (lane4 & 0x10u) { uint32_t t = u0; u0 = u1; u1 = u2; u2 = u3; u3 = t; }
+        const uint32_t s8 = (lane4 & 0xcu) << 1;
+        const uint32_t v[4] = {__builtin_amdgcn_alignbit(u1, u0, s8),
+                               __builtin_amdgcn_alignbit(u2, u1, s8),
+                               __builtin_amdgcn_alignbit(u3, u2, s8),
+                               __builtin_amdgcn_alignbit(u0, u3, s8)};
+        const uint32_t j[4] = {jt.x, jt.y, jt.z, jt.w};
+        uint4 e[16];
+#pragma unroll
+        for (int t = 0; t < 16; ++t) {
+            const uint32_t sel = 0x0c0c0000u | ((4u + (t & 3)) << 8) | (uint32_t)(t & 3);
+            e[t] = lds_u128(__builtin_amdgcn_perm(v[t >> 2], j[t >> 2], sel));
         }
         uint4 z = xor4_3(e[0], e[1], e[2]);
         z = xor4_3(z, e[3], e[4]);
@@ -298,25 +335,44 @@ __device__ __forceinline__ void gcm_record(const tg_batch& b, uint64_t i, uint32
 }
 
 
-template <int NR, bool OPEN, int G, int THREADS, bool ROT>
+// GHASH flavours of the single-key kernel: 0 = GhashTables, 1 = GhashTablesRot,
+// 2 = GhashTablesRotLds.
+template <int NR, bool OPEN, int G, int THREADS, int GH>
 __global__ __launch_bounds__(THREADS) void gcm_kernel(const GcmKeyDev* __restrict__ key,
                                                       tg_batch b) {
+    constexpr bool ROT = GH != 0;
     uint4* lds = g_lds;
     // stage the GHASH tables (ROT: row layout b * 16 + j) and the Te0/Te2 copies
     for (int e = threadIdx.x; e < kGhashEntries; e += blockDim.x)
         lds[ROT ? (e & 255) * 16 + (e >> 8) : e] = key->ghash[e];
+    if (GH == 2 && threadIdx.x < 16) {   // row l: byte k of word q = ((l + 4q + k) % 16) * 16
+        uint32_t w[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            w[q] = 0;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) w[q] |= (((threadIdx.x + 4 * q + k) & 15u) << 4) << (8 * k);
+        }
+        lds[kJtBase / 16 + threadIdx.x] = make_uint4(w[0], w[1], w[2], w[3]);
+    }
     stage_te(reinterpret_cast<uint32_t*>(lds) + kTeBase / 4);
     RkRegs<NR> rk;
 #pragma unroll
     for (int k = 0; k < 4 * (NR + 1); ++k) rk.w[k] = key->rk[k];
-    typename std::conditional<ROT, GhashTablesRot, GhashTables>::type gh;
-    if constexpr (ROT) gh.init(threadIdx.x & 63);
     __syncthreads();
 
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= b.n) return;
     const uint32_t lane4 = ((threadIdx.x & 31u) << 2) | kTeBase;
-    gcm_record<NR, OPEN, G>(b, i, lane4, rk, gh);
+    if constexpr (GH == 0) {
+        gcm_record<NR, OPEN, G>(b, i, lane4, rk, GhashTables{});
+    } else if constexpr (GH == 1) {
+        GhashTablesRot gh;
+        gh.init(threadIdx.x & 63);
+        gcm_record<NR, OPEN, G>(b, i, lane4, rk, gh);
+    } else {
+        gcm_record<NR, OPEN, G>(b, i, lane4, rk, GhashTablesRotLds{lane4});
+    }
 }
 
 // Key-table kernel (many sessions per batch, BASELINE config 4): lane i uses
@@ -344,18 +400,18 @@ __global__ __launch_bounds__(kMkThreads, 4) void gcm_table_kernel(const GcmTable
     gcm_record<NR, OPEN, G>(b, i, lane4, rk, gh);
 }
 
-template <int NR, bool OPEN, int G, int THREADS, bool ROT>
+template <int NR, bool OPEN, int G, int THREADS, int GH>
 int launch_v(const GcmKeyDev* key, const tg_batch& b, hipStream_t s) {
     static bool attr_set = false;
     if (!attr_set) {
-        if (hipFuncSetAttribute((const void*)gcm_kernel<NR, OPEN, G, THREADS, ROT>,
+        if (hipFuncSetAttribute((const void*)gcm_kernel<NR, OPEN, G, THREADS, GH>,
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)kGcmLds) !=
             hipSuccess)
             return TG_EHIP;
         attr_set = true;
     }
     const uint64_t blocks = (b.n + THREADS - 1) / THREADS;
-    hipLaunchKernelGGL((gcm_kernel<NR, OPEN, G, THREADS, ROT>), dim3((unsigned)blocks), dim3(THREADS),
+    hipLaunchKernelGGL((gcm_kernel<NR, OPEN, G, THREADS, GH>), dim3((unsigned)blocks), dim3(THREADS),
                        kGcmLds, s, key, b);
     return hipGetLastError() == hipSuccess ? TG_OK : TG_EHIP;
 }
@@ -374,11 +430,17 @@ int variant() {
 template <int NR, bool OPEN>
 int launch(const GcmKeyDev* key, const tg_batch& b, hipStream_t s) {
     switch (variant()) {
-        case 1: return launch_v<NR, OPEN, 4, 1024, false>(key, b, s);
-        case 2: return launch_v<NR, OPEN, 2, 1024, true>(key, b, s);
-        case 3: return launch_v<NR, OPEN, 1, 1024, true>(key, b, s);
-        case 4: return launch_v<NR, OPEN, 2, 512, true>(key, b, s);
-        default: return launch_v<NR, OPEN, 2, 1024, false>(key, b, s);
+        case 1: return launch_v<NR, OPEN, 4, 1024, 0>(key, b, s);
+        case 2: return launch_v<NR, OPEN, 2, 1024, 1>(key, b, s);
+        case 3: return launch_v<NR, OPEN, 1, 1024, 1>(key, b, s);
+        case 4: return launch_v<NR, OPEN, 2, 512, 1>(key, b, s);
+        case 5: return launch_v<NR, OPEN, 2, 1024, 2>(key, b, s);
+        case 6: return launch_v<NR, OPEN, 4, 1024, 2>(key, b, s);
+        case 7: return launch_v<NR, OPEN, 2, 768, 2>(key, b, s);
+        case 8: return launch_v<NR, OPEN, 2, 768, 1>(key, b, s);
+        case 9: return launch_v<NR, OPEN, 4, 768, 0>(key, b, s);
+        case 10: return launch_v<NR, OPEN, 4, 768, 2>(key, b, s);
+        default: return launch_v<NR, OPEN, 2, 1024, 0>(key, b, s);
     }
 }
 
