@@ -178,6 +178,25 @@ typedef struct tg_records {
 int tg_seal_records(tg_key* k, const tg_records* r, void* stream);
 int tg_open_records(tg_key* k, const tg_records* r, void* stream);
 
+/* Bulk TLS 1.3 key setup on the device -- the
+ * per-session work of RecordLayer.calcTLS1_3PendingState
+ * (recordlayer.py:1268-1323) and _calcTLS1_3KeyUpdate (:1325-1350) for many
+ * sessions at once, all buffers DEVICE pointers.
+ * tg_hkdf_expand_label: out[i] = HKDF-Expand-Label(secrets[i], label,
+ *   context, outlen) (cryptomath.py:155-173, HKDF_expand :146-153, HMAC
+ *   :128-132) for i < n; hashlen 32 (SHA-256) or 48 (SHA-384) is both the
+ *   PRF and the secret size; 1 <= outlen <= hashlen (every record-layer use:
+ *   "key", "iv", "traffic upd", "finished").  Secrets at hashlen * i, outputs
+ *   at outlen * i.
+ * tg_key_create_device: tg_key_create with the keys (nkeys x keylen) already
+ *   in device memory: the AES key schedule, H = E_K(0) and the GHASH tables
+ *   are built by kernels on `stream` (synchronised before returning), so
+ *   derived keys never visit the host. */
+int tg_hkdf_expand_label(int hashlen, const uint8_t* secrets, uint64_t n, const uint8_t* label,
+                         size_t labellen, const uint8_t* context, size_t ctxlen, size_t outlen,
+                         uint8_t* out, void* stream);
+int tg_key_create_device(int alg, const uint8_t* keys, size_t keylen, size_t nkeys,
+                         tg_key** out, void* stream);
 /* Device memory helpers so a ctypes host needs no other GPU runtime. */
 int tg_malloc(void** p, size_t bytes);
 int tg_free(void* p);

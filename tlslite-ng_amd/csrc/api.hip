@@ -349,6 +349,71 @@ int records(tg_key* k, const tg_records* r, void* stream, bool seal) {
     return TG_OK;
 }
 
+// Validate (alg, keylen, nkeys) and allocate a handle with its stream.
+int new_key(int alg, size_t keylen, size_t nkeys, tg_key** out) {
+    *out = nullptr;
+    if (alg == TG_AES_GCM || is_ccm(alg)) {
+        // AssertionError in AESGCM.__init__ (aesgcm.py:37-38) and AESCCM.__init__ (aesccm.py:22-30)
+        if (keylen != 16 && keylen != 32) return fail(TG_EKEYLEN, "AES key must be 16 or 32 bytes");
+    } else if (alg == TG_CHACHA20_POLY1305) {
+        if (keylen != 32) return fail(TG_EKEYLEN, "Key must be 256 bit long");
+    } else {
+        return fail(TG_EINVAL, "unknown algorithm %d", alg);
+    }
+    int dev = 0;
+    HIP_TRY(hipGetDevice(&dev));
+    tg_key* k = new (std::nothrow) tg_key();
+    if (!k) return fail(TG_ENOMEM, "out of host memory");
+    k->alg = alg;
+    k->keylen = keylen;
+    k->nkeys = nkeys;
+    k->taglen = alg == TG_AES_CCM_8 ? 8 : 16;
+    k->rounds = alg == TG_CHACHA20_POLY1305 ? 0 : (keylen == 16 ? 10 : 14);
+    k->device = dev;
+    hipError_t e = hipStreamCreateWithFlags(&k->stream, hipStreamNonBlocking);
+    if (e != hipSuccess) {
+        delete k;
+        return fail(TG_EHIP, "hipStreamCreate: %s", hipGetErrorString(e));
+    }
+    *out = k;
+    return TG_OK;
+}
+
+// HkdfLabel (cryptomath.py:155-173) || 0x01, SHA-padded after one key block.
+int hkdf_message(int hashlen, const uint8_t* label, size_t labellen, const uint8_t* ctx,
+                 size_t ctxlen, size_t outlen, tg::HkdfMsg& msg) {
+    uint8_t m[256];
+    size_t n = 0;
+    if (6 + labellen > 255 || ctxlen > 255) return fail(TG_EINVAL, "label or context too long");
+    m[n++] = (uint8_t)(outlen >> 8);                     // addTwo(length)
+    m[n++] = (uint8_t)outlen;
+    m[n++] = (uint8_t)(6 + labellen);                    // addVarSeq("tls13 " + label, 1, 1)
+    memcpy(m + n, "tls13 ", 6);
+    n += 6;
+    if (n + labellen + 2 + ctxlen > 200) return fail(TG_EINVAL, "label or context too long");
+    memcpy(m + n, label, labellen);
+    n += labellen;
+    m[n++] = (uint8_t)ctxlen;                            // addVarSeq(hashValue, 1, 1)
+    if (ctxlen) memcpy(m + n, ctx, ctxlen);
+    n += ctxlen;
+    m[n++] = 1;                                          // HKDF_expand block counter x = 1
+    const size_t block = hashlen == 32 ? 64 : 128, lenfield = hashlen == 32 ? 8 : 16;
+    const uint64_t bits = (uint64_t)(block + n) * 8;     // the (K ^ ipad) block comes first
+    size_t total = (n + 1 + lenfield + block - 1) / block * block;
+    if (total > sizeof(msg.words)) return fail(TG_EINVAL, "label or context too long");
+    uint8_t buf[256] = {0};
+    memcpy(buf, m, n);
+    buf[n] = 0x80;
+    for (int k = 0; k < 8; ++k) buf[total - 1 - k] = (uint8_t)(bits >> (8 * k));
+    memset(&msg, 0, sizeof(msg));
+    msg.nblocks = (uint32_t)(total / block);
+    msg.outlen = (uint32_t)outlen;
+    for (size_t w = 0; w < total / 4; ++w)
+        msg.words[w] = ((uint32_t)buf[4 * w] << 24) | ((uint32_t)buf[4 * w + 1] << 16) |
+                       ((uint32_t)buf[4 * w + 2] << 8) | buf[4 * w + 3];
+    return TG_OK;
+}
+
 }  // namespace
 
 extern "C" {
@@ -380,30 +445,10 @@ int tg_init(int device) {
 
 int tg_key_create(int alg, const uint8_t* keys, size_t keylen, size_t nkeys, tg_key** out) {
     if (!out || !keys || nkeys == 0) return fail(TG_EINVAL, "null argument");
-    *out = nullptr;
-    if (alg == TG_AES_GCM || is_ccm(alg)) {
-        // AssertionError in AESGCM.__init__ (aesgcm.py:37-38) and AESCCM.__init__ (aesccm.py:22-30)
-        if (keylen != 16 && keylen != 32) return fail(TG_EKEYLEN, "AES key must be 16 or 32 bytes");
-    } else if (alg == TG_CHACHA20_POLY1305) {
-        if (keylen != 32) return fail(TG_EKEYLEN, "Key must be 256 bit long");
-    } else {
-        return fail(TG_EINVAL, "unknown algorithm %d", alg);
-    }
-    int dev = 0;
-    HIP_TRY(hipGetDevice(&dev));
-    tg_key* k = new (std::nothrow) tg_key();
-    if (!k) return fail(TG_ENOMEM, "out of host memory");
-    k->alg = alg;
-    k->keylen = keylen;
-    k->nkeys = nkeys;
-    k->taglen = alg == TG_AES_CCM_8 ? 8 : 16;
-    k->device = dev;
-    int rc = TG_OK;
-    hipError_t e = hipStreamCreateWithFlags(&k->stream, hipStreamNonBlocking);
-    if (e != hipSuccess) {
-        delete k;
-        return fail(TG_EHIP, "hipStreamCreate: %s", hipGetErrorString(e));
-    }
+    tg_key* k = nullptr;
+    int rc = new_key(alg, keylen, nkeys, &k);
+    if (rc) return rc;
+    hipError_t e = hipSuccess;
     if (is_ccm(alg)) {
         tg::AesKeyDev* hk = new (std::nothrow) tg::AesKeyDev[nkeys];
         if (!hk) rc = fail(TG_ENOMEM, "out of host memory");
@@ -496,6 +541,52 @@ int tg_key_create(int alg, const uint8_t* keys, size_t keylen, size_t nkeys, tg_
     *out = k;
     return TG_OK;
 }
+
+int tg_key_create_device(int alg, const uint8_t* keys, size_t keylen, size_t nkeys,
+                         tg_key** out, void* stream) {
+    if (!out || !keys || nkeys == 0) return fail(TG_EINVAL, "null argument");
+    tg_key* k = nullptr;
+    int rc = new_key(alg, keylen, nkeys, &k);
+    if (rc) return rc;
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    const size_t bytes = dev_key_bytes(k);
+    hipError_t e = hipMalloc(&k->dev_key, bytes);
+    if (e != hipSuccess) {
+        rc = fail(TG_EHIP, "key alloc: %s", hipGetErrorString(e));
+    } else if (alg == TG_CHACHA20_POLY1305) {   // ChachaKeyDev is the raw key bytes (LE words)
+        e = hipMemcpyAsync(k->dev_key, keys, 32 * nkeys, hipMemcpyDeviceToDevice, st);
+        if (e != hipSuccess) rc = fail(TG_EHIP, "key copy: %s", hipGetErrorString(e));
+    } else {
+        const int layout = is_ccm(alg) ? 2 : (nkeys > 1 ? 1 : 0);
+        rc = tg_launch_aes_setup((int)keylen, layout, keys, nkeys, k->dev_key, st);
+        if (rc) rc = fail(rc, "key setup launch failed");
+    }
+    if (!rc && (e = hipStreamSynchronize(st)) != hipSuccess)
+        rc = fail(TG_EHIP, "key setup: %s", hipGetErrorString(e));
+    if (rc) {
+        tg_key_destroy(k);
+        return rc;
+    }
+    *out = k;
+    return TG_OK;
+}
+
+int tg_hkdf_expand_label(int hashlen, const uint8_t* secrets, uint64_t n, const uint8_t* label,
+                         size_t labellen, const uint8_t* context, size_t ctxlen, size_t outlen,
+                         uint8_t* out, void* stream) {
+    if (hashlen != 32 && hashlen != 48) return fail(TG_EINVAL, "hash length must be 32 or 48");
+    if (outlen == 0 || outlen > (size_t)hashlen)
+        return fail(TG_EINVAL, "output length must be 1..%d", hashlen);
+    if ((labellen && !label) || (ctxlen && !context)) return fail(TG_EINVAL, "null label");
+    if (n == 0) return TG_OK;
+    if (!secrets || !out) return fail(TG_EINVAL, "null device buffer");
+    tg::HkdfMsg msg;
+    int rc = hkdf_message(hashlen, label, labellen, context, ctxlen, outlen, msg);
+    if (rc) return rc;
+    rc = tg_launch_hkdf(hashlen, msg, secrets, n, out, static_cast<hipStream_t>(stream));
+    return rc ? fail(rc, "hkdf launch failed") : TG_OK;
+}
+
 
 int tg_key_destroy(tg_key* k) {
     if (!k) return TG_OK;

@@ -112,6 +112,15 @@ __device__ __forceinline__ uint4 mask_tail(uint4 v, uint32_t n) {
     return make_uint4(w[0], w[1], w[2], w[3]);
 }
 
+// The session-independent part of an HKDF-Expand-Label call (keysetup.hip):
+// info || 0x01 and its SHA padding, as big-endian 32-bit words of the message
+// blocks that follow the (K ^ ipad) block.
+struct HkdfMsg {
+    uint32_t nblocks;     // SHA-256: 64-byte blocks (16 words); SHA-384: 128-byte (32 words)
+    uint32_t outlen;      // bytes kept of T(1), <= hash length
+    uint32_t words[64];
+};
+
 // Per-call device scratch of the record-framing entry points (records.hip).
 struct RecScratch {
     uint64_t* in_abs;     // AEAD input address per record (open)
@@ -138,5 +147,9 @@ int tg_launch_chacha(const tg::ChachaKeyDev* keys, const tg_batch& b, bool open,
 int tg_launch_records_prep(const tg_records& r, bool seal, bool aes, int taglen,
                            const tg::RecScratch& s, hipStream_t st);
 int tg_launch_records_finish(const tg_records& r, const tg::RecScratch& s, hipStream_t st);
+int tg_launch_hkdf(int hashlen, const tg::HkdfMsg& msg, const uint8_t* secrets, uint64_t n,
+                   uint8_t* out, hipStream_t s);
+int tg_launch_aes_setup(int keylen, int layout, const uint8_t* keys, uint64_t n, void* out,
+                        hipStream_t s);
 int tg_launch_nonces(int mode, const uint8_t* iv_host, uint64_t seq0, uint64_t n, uint8_t* out,
                      hipStream_t s);

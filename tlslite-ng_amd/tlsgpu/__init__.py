@@ -12,5 +12,6 @@ from .batch import KeyTable, make_batch, make_nonces, open_batch, seal_batch  # 
 from .cipherfactory import (CIPHER_IMPLEMENTATIONS, createAESCCM, createAESCCM_8,  # noqa: F401
                             createAESGCM, createCHACHA20)
 from .records import TLS12, TLS13, open_records, seal_records  # noqa: F401
+from . import keysetup  # noqa: F401
 
 __version__ = "0.1.0"

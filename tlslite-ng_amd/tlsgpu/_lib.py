@@ -27,7 +27,8 @@ TG_AES_CCM_8 = 3
 EXPORTS = ("tg_version", "tg_last_error", "tg_device_count", "tg_init", "tg_key_create",
            "tg_key_destroy", "tg_key_info", "tg_key_taglen", "tg_seal", "tg_open", "tg_seal_batch",
            "tg_open_batch", "tg_make_nonces", "tg_malloc", "tg_free", "tg_memcpy_h2d",
-           "tg_memcpy_d2h", "tg_stream_sync", "tg_seal_records", "tg_open_records")
+           "tg_memcpy_d2h", "tg_stream_sync", "tg_seal_records", "tg_open_records",
+           "tg_hkdf_expand_label", "tg_key_create_device")
 
 TG_TLS12 = 0x0303
 TG_TLS13 = 0x0304
@@ -117,6 +118,8 @@ def load():
     l.tg_make_nonces.argtypes = [i, p, sz, u64, u64, p, p]
     l.tg_seal_records.argtypes = [p, ctypes.POINTER(TgRecords), p]
     l.tg_open_records.argtypes = [p, ctypes.POINTER(TgRecords), p]
+    l.tg_hkdf_expand_label.argtypes = [i, p, u64, p, sz, p, sz, sz, p, p]
+    l.tg_key_create_device.argtypes = [i, p, sz, sz, ctypes.POINTER(ctypes.c_void_p), p]
     l.tg_malloc.argtypes = [ctypes.POINTER(ctypes.c_void_p), sz]
     l.tg_free.argtypes = [p]
     l.tg_memcpy_h2d.argtypes = [p, p, sz, p]

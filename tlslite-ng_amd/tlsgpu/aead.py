@@ -20,10 +20,14 @@ from . import _lib
 class _DeviceKey(object):
     """Refcounted owner of one ``tg_key`` handle (freed when unreferenced)."""
 
-    def __init__(self, alg, key, nkeys=1):
+    def __init__(self, alg, key, nkeys=1, device_keys=None, keylen=0, stream=None):
         lib = _lib.load()
         self._lib = lib
         self.handle = ctypes.c_void_p()
+        if device_keys is not None:   # keys already in HBM (tg_key_create_device)
+            _lib.check(lib.tg_key_create_device(alg, device_keys, keylen, nkeys,
+                                                ctypes.byref(self.handle), stream))
+            return
         raw = bytes(key)
         _lib.check(lib.tg_key_create(alg, raw, len(raw) // nkeys, nkeys,
                                      ctypes.byref(self.handle)))

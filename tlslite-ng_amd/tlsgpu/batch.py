@@ -48,6 +48,10 @@ def _stream(stream):
     return stream.cuda_stream
 
 
+ALG_CODES = {"aesgcm": _lib.TG_AES_GCM, "aesccm": _lib.TG_AES_CCM,
+             "aesccm_8": _lib.TG_AES_CCM_8, "chacha20-poly1305": _lib.TG_CHACHA20_POLY1305}
+
+
 class KeyTable(object):
     """Many session keys of one algorithm, indexed by ``key_idx`` in a batch."""
 
@@ -55,13 +59,22 @@ class KeyTable(object):
         keys = [bytes(k) for k in keys]
         if not keys or len(set(len(k) for k in keys)) != 1:
             raise ValueError("keys must be a non-empty list of equal-length keys")
-        code = {"aesgcm": _lib.TG_AES_GCM, "aesccm": _lib.TG_AES_CCM,
-                "aesccm_8": _lib.TG_AES_CCM_8,
-                "chacha20-poly1305": _lib.TG_CHACHA20_POLY1305}[alg]
         self.alg = alg
         self.nkeys = len(keys)
+        self.keylen = len(keys[0])
         self.tagLength = 8 if alg == "aesccm_8" else 16
-        self._dkey = _DeviceKey(code, b"".join(keys), len(keys))
+        self._dkey = _DeviceKey(ALG_CODES[alg], b"".join(keys), len(keys))
+
+    @classmethod
+    def from_device(cls, alg, keys, nkeys, keylen, stream=None):
+        """Key table from ``nkeys`` x ``keylen`` key bytes already in device
+        memory (tg_key_create_device: schedule, H and tables built on the GPU)."""
+        t = cls.__new__(cls)
+        t.alg, t.nkeys, t.keylen = alg, int(nkeys), int(keylen)
+        t.tagLength = 8 if alg == "aesccm_8" else 16
+        t._dkey = _DeviceKey(ALG_CODES[alg], None, t.nkeys, device_keys=_ptr(keys, "keys"),
+                             keylen=t.keylen, stream=_stream(stream))
+        return t
 
 
 def _handle(key):
