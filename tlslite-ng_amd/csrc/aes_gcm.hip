@@ -240,7 +240,10 @@ struct GhashClmul {  // y kept in normal order; hn = H in normal order
 // g+1 and the payload of group g+1 are produced while group g is XORed and
 // hashed, so the GHASH chain of seal (which needs the ciphertext) overlaps the
 // next group's AES rounds.
-template <int NR, bool OPEN, bool ALIGNED, int G, class RK, class GH>
+// SPLIT: a scheduling fence between the AES of group g+1 and the GHASH of
+// group g, so their register peaks do not add up (the waves' own
+// interleaving still overlaps the two).
+template <int NR, bool OPEN, bool ALIGNED, int G, int SPLIT, class RK, class GH>
 __device__ __forceinline__ uint4 ctr_groups(uint32_t lane4, const RK& rk, const GH& gh,
                                             const CtrCache& cc, const uint8_t* in, uint8_t* out,
                                             uint32_t ngroups, uint4 y) {
@@ -262,6 +265,7 @@ __device__ __forceinline__ uint4 ctr_groups(uint32_t lane4, const RK& rk, const 
         }
 #pragma unroll
         for (int q = 0; q < G; ++q) ks[q] = aes_ctr<NR>(lane4, rk, cc, 2u + G * (g + 1) + q);
+        if (SPLIT) __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
         for (int q = 0; q < G; ++q) y = gh.update(y, OPEN ? d[q] : c[q]);
 #pragma unroll
@@ -271,7 +275,7 @@ __device__ __forceinline__ uint4 ctr_groups(uint32_t lane4, const RK& rk, const 
 }
 
 // One record: AESGCM.seal / AESGCM.open (aesgcm.py:101-154) for lane i.
-template <int NR, bool OPEN, int G, class RK, class GH>
+template <int NR, bool OPEN, int G, class RK, class GH, int SPLIT = 0>
 __device__ __forceinline__ void gcm_record(const tg_batch& b, uint64_t i, uint32_t lane4,
                                            const RK& rk, const GH& gh) {
     const uint8_t* in = rec_in(b, i);
@@ -297,8 +301,8 @@ __device__ __forceinline__ void gcm_record(const tg_batch& b, uint64_t i, uint32
     const uint32_t nfull = len >> 4;
     const uint32_t tail = len & 15;
     const uint32_t ngroups = nfull / G;
-    y = aligned ? ctr_groups<NR, OPEN, true, G>(lane4, rk, gh, cc, in, out, ngroups, y)
-                : ctr_groups<NR, OPEN, false, G>(lane4, rk, gh, cc, in, out, ngroups, y);
+    y = aligned ? ctr_groups<NR, OPEN, true, G, SPLIT>(lane4, rk, gh, cc, in, out, ngroups, y)
+                : ctr_groups<NR, OPEN, false, G, SPLIT>(lane4, rk, gh, cc, in, out, ngroups, y);
     for (uint32_t j = G * ngroups; j < nfull; ++j) {
         const uint4 ks = aes_ctr<NR>(lane4, rk, cc, 2u + j);
         const uint4 d = load16(in + 16 * j, aligned);
@@ -335,17 +339,18 @@ __device__ __forceinline__ void gcm_record(const tg_batch& b, uint64_t i, uint32
 }
 
 
-// GHASH flavours of the single-key kernel: 0 = GhashTables, 1 = GhashTablesRot,
-// 2 = GhashTablesRotLds.
+// GHASH flavours of the single-key kernel (GH % 10): 0 = GhashTables,
+// 1 = GhashTablesRot, 2 = GhashTablesRotLds; GH / 10 = 1 adds the SPLIT fence.
 template <int NR, bool OPEN, int G, int THREADS, int GH>
 __global__ __launch_bounds__(THREADS) void gcm_kernel(const GcmKeyDev* __restrict__ key,
                                                       tg_batch b) {
-    constexpr bool ROT = GH != 0;
+    constexpr int GHK = GH % 10, SPLIT = GH / 10;   // GHASH flavour, split schedule
+    constexpr bool ROT = GHK != 0;
     uint4* lds = g_lds;
     // stage the GHASH tables (ROT: row layout b * 16 + j) and the Te0/Te2 copies
     for (int e = threadIdx.x; e < kGhashEntries; e += blockDim.x)
         lds[ROT ? (e & 255) * 16 + (e >> 8) : e] = key->ghash[e];
-    if (GH == 2 && threadIdx.x < 16) {   // row l: byte k of word q = ((l + 4q + k) % 16) * 16
+    if (GHK == 2 && threadIdx.x < 16) {   // row l: byte k of word q = ((l + 4q + k) % 16) * 16
         uint32_t w[4];
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
@@ -364,14 +369,15 @@ __global__ __launch_bounds__(THREADS) void gcm_kernel(const GcmKeyDev* __restric
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= b.n) return;
     const uint32_t lane4 = ((threadIdx.x & 31u) << 2) | kTeBase;
-    if constexpr (GH == 0) {
-        gcm_record<NR, OPEN, G>(b, i, lane4, rk, GhashTables{});
-    } else if constexpr (GH == 1) {
+    if constexpr (GHK == 0) {
+        gcm_record<NR, OPEN, G, RkRegs<NR>, GhashTables, SPLIT>(b, i, lane4, rk, GhashTables{});
+    } else if constexpr (GHK == 1) {
         GhashTablesRot gh;
         gh.init(threadIdx.x & 63);
-        gcm_record<NR, OPEN, G>(b, i, lane4, rk, gh);
+        gcm_record<NR, OPEN, G, RkRegs<NR>, GhashTablesRot, SPLIT>(b, i, lane4, rk, gh);
     } else {
-        gcm_record<NR, OPEN, G>(b, i, lane4, rk, GhashTablesRotLds{lane4});
+        gcm_record<NR, OPEN, G, RkRegs<NR>, GhashTablesRotLds, SPLIT>(b, i, lane4, rk,
+                                                                     GhashTablesRotLds{lane4});
     }
 }
 
@@ -416,8 +422,9 @@ int launch_v(const GcmKeyDev* key, const tg_batch& b, hipStream_t s) {
     return hipGetLastError() == hipSuccess ? TG_OK : TG_EHIP;
 }
 
-// Tuning variants (TLSGPU_GCM_VARIANT, for measurement only): blocks per
-// iteration x threads per workgroup.
+// Tuning variants (TLSGPU_GCM_VARIANT, for measurement only): blocks per lane
+// iteration G x threads per workgroup x GHASH flavour.  Default: G = 4, 1024
+// threads, 8-bit tables (fastest measured; profiles/r01/gcm_variant_sweep.txt).
 int variant() {
     static int v = -1;
     if (v < 0) {
@@ -429,18 +436,11 @@ int variant() {
 
 template <int NR, bool OPEN>
 int launch(const GcmKeyDev* key, const tg_batch& b, hipStream_t s) {
-    switch (variant()) {
-        case 1: return launch_v<NR, OPEN, 4, 1024, 0>(key, b, s);
-        case 2: return launch_v<NR, OPEN, 2, 1024, 1>(key, b, s);
-        case 3: return launch_v<NR, OPEN, 1, 1024, 1>(key, b, s);
-        case 4: return launch_v<NR, OPEN, 2, 512, 1>(key, b, s);
-        case 5: return launch_v<NR, OPEN, 2, 1024, 2>(key, b, s);
-        case 6: return launch_v<NR, OPEN, 4, 1024, 2>(key, b, s);
-        case 7: return launch_v<NR, OPEN, 2, 768, 2>(key, b, s);
-        case 8: return launch_v<NR, OPEN, 2, 768, 1>(key, b, s);
-        case 9: return launch_v<NR, OPEN, 4, 768, 0>(key, b, s);
-        case 10: return launch_v<NR, OPEN, 4, 768, 2>(key, b, s);
-        default: return launch_v<NR, OPEN, 2, 1024, 0>(key, b, s);
+    switch (variant()) {   // profiles/r01/gcm_variant_sweep.txt
+        case 1: return launch_v<NR, OPEN, 2, 1024, 0>(key, b, s);
+        case 2: return launch_v<NR, OPEN, 2, 1024, 2>(key, b, s);
+        case 3: return launch_v<NR, OPEN, 2, 512, 1>(key, b, s);
+        default: return launch_v<NR, OPEN, 4, 1024, 0>(key, b, s);
     }
 }
 
