@@ -93,6 +93,9 @@ def main():
     ap.add_argument("--cpu-records", type=int, default=6)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--e2e", action="store_true", help="also time the host<->device path")
+    ap.add_argument("--traffic-file", default=os.path.join(ROOT, "profiles", "r01", "traffic.json"),
+                    help="per-launch HBM bytes from tools/traffic.sh (rocprofv3 FETCH_SIZE / "
+                         "WRITE_SIZE passes at this config) for roofline.traffic")
     ap.add_argument("--record-align", type=int, default=128,
                     help="byte alignment of each sealed record (ct||tag) in the packed batch")
     ap.add_argument("--config", default="headline", choices=["headline", "c4", "c5"],
@@ -215,8 +218,10 @@ def main():
             "per_kernel": per_kernel,
             "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(dom_achieved, 1),
                          "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(dom_achieved / HBM_PEAK_GBS, 4), "traffic": None,
-                         "bytes_per_record": algorithmic_bytes(1, L, dom_op)},
+                         "frac": round(dom_achieved / HBM_PEAK_GBS, 4),
+                         "traffic": measured_traffic(args.traffic_file, dom, n, L),
+                         "bytes_per_record": algorithmic_bytes(1, L, dom_op),
+                         "algorithmic_bytes_per_launch": algorithmic_bytes(n, L, dom_op)},
             "verified": bool(ok),
             "auth_failures": int(sums[2]),
         }
@@ -229,6 +234,17 @@ def main():
         dist.destroy_process_group()
     if not ok:
         sys.exit(3)
+
+
+def measured_traffic(path, kernel, n, L):
+    """HBM bytes per launch of ``kernel`` from a committed tools/traffic.sh
+    summary (PMC passes cannot run inside the timed process), or None when
+    there is none for this exact config (2^20 x 16 KiB headline records)."""
+    if n != 1 << 20 or L != 16384 or not os.path.exists(path):
+        return None
+    with open(path) as f:
+        t = json.load(f)
+    return round(t[kernel]["hbm_bytes"]) if kernel in t else None
 
 
 def init_dist(torch, dist):
