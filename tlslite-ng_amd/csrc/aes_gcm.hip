@@ -23,6 +23,7 @@
 #include <type_traits>
 
 #include "aes_round.h"
+#include "aes_bs.h"
 
 namespace tg {
 namespace {
@@ -63,6 +64,32 @@ __device__ __forceinline__ uint4 gmul(uint4 y) {
     z = xor4_3(z, e[11], e[12]);
     z = xor4_3(z, e[13], e[14]);
     return xor4(z, e[15]);
+}
+
+// gmul with at most eight table rows in flight (32 VGPRs instead of 64), for
+// the bitsliced kernel whose keystream chunk already holds 128 VGPRs.
+__device__ __forceinline__ uint4 gmul_lowreg(uint4 y) {
+    const uint32_t w[4] = {y.x, y.y, y.z, y.w};
+    uint4 z = make_uint4(0, 0, 0, 0);
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        uint4 e[8];
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+            const uint32_t v = w[2 * h + q];
+            const int t = 4 * (2 * h + q);
+            e[4 * q + 0] = lds_u128(((v << 4) & 0xff0u) + 4096 * (t + 0));
+            e[4 * q + 1] = lds_u128(((v >> 4) & 0xff0u) + 4096 * (t + 1));
+            e[4 * q + 2] = lds_u128(((v >> 12) & 0xff0u) + 4096 * (t + 2));
+            e[4 * q + 3] = lds_u128(((v >> 20) & 0xff0u) + 4096 * (t + 3));
+        }
+        z = xor4_3(z, e[0], e[1]);
+        z = xor4_3(z, e[2], e[3]);
+        z = xor4_3(z, e[4], e[5]);
+        z = xor4_3(z, e[6], e[7]);
+        __builtin_amdgcn_sched_barrier(0);
+    }
+    return z;
 }
 
 struct GhashTables {  // single key: the 8-bit tables staged in LDS; y in block byte layout
@@ -381,6 +408,356 @@ __global__ __launch_bounds__(THREADS) void gcm_kernel(const GcmKeyDev* __restric
     }
 }
 
+// ---- bitsliced single-key kernel ---------------------------------------
+// AES on the VALU (aes_bs.h): each lane runs its record in chunks of 32
+// counter blocks, 2 + 32 j ... 33 + 32 j, bitsliced across the 32 bits of
+// every register; the wave walks the chunks in lock step (j is wave-uniform,
+// so the counter planes are scalar), up to the longest record of the wave.
+// LDS holds only the GHASH tables (64 KiB) and a 256-byte S-box for the
+// per-record work: the first-round S-box of the nonce bytes, the tag mask
+// E_K(J0) and the keystream of a trailing partial block, which are single
+// blocks done with a byte-wise AES (aes_block_sb).  512 threads = two waves
+// per SIMD (the cipher keeps 128 state planes + S-box temporaries live).
+constexpr int kBsThreads = 512;
+constexpr uint32_t kSboxBase = 65536;
+// GHASH staging (hooked path): per wave two buffers of 4 blocks x 64 lanes x 16 B
+constexpr uint32_t kStageBase = 65536 + 256;
+constexpr uint32_t kStageWave = 2 * 4 * 1024;
+constexpr size_t kBsLds = kStageBase + (kBsThreads / 64) * kStageWave;
+
+#if defined(__HIP_DEVICE_COMPILE__)
+__device__ __forceinline__ uint32_t lds_u8(uint32_t addr) {
+    return *(const __attribute__((address_space(3))) uint8_t*)(uintptr_t)addr;
+}
+#else
+__device__ __forceinline__ uint32_t lds_u8(uint32_t) { return 0; }
+#endif
+
+// S-box of each byte of w (LDS table at kSboxBase)
+__device__ __forceinline__ uint32_t sub_word(uint32_t w) {
+    return lds_u8(kSboxBase + (w & 0xffu)) | (lds_u8(kSboxBase + ((w >> 8) & 0xffu)) << 8) |
+           (lds_u8(kSboxBase + ((w >> 16) & 0xffu)) << 16) | (lds_u8(kSboxBase + (w >> 24)) << 24);
+}
+
+// MixColumns of one column packed as a LE word (byte i = row i):
+// out_i = 2 (a_i ^ a_i+1) ^ a_i+1 ^ a_i+2 ^ a_i+3.
+__device__ __forceinline__ uint32_t mix_word(uint32_t w) {
+    const uint32_t r1 = __builtin_amdgcn_alignbit(w, w, 8), r2 = __builtin_amdgcn_alignbit(w, w, 16),
+                   r3 = __builtin_amdgcn_alignbit(w, w, 24);
+    const uint32_t u = w ^ r1;
+    const uint32_t xt = ((u & 0x7f7f7f7fu) << 1) ^ (((u >> 7) & 0x01010101u) * 0x1bu);
+    return xt ^ xor3(r1, r2, r3);
+}
+
+// One block, byte-wise (rijndael.py:995-1038 restated): state words are the
+// columns, ShiftRows takes row i of column c from column (c + i) % 4.
+template <int NR>
+__device__ __forceinline__ uint4 aes_block_sb(const uint32_t* rk, uint4 in) {
+    uint32_t s[4] = {in.x ^ rk[0], in.y ^ rk[1], in.z ^ rk[2], in.w ^ rk[3]};
+#pragma unroll 1
+    for (int r = 1; r <= NR; ++r) {
+        uint32_t t[4];
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            const uint32_t w = __builtin_amdgcn_perm(s[(c + 1) & 3], s[c], 0x07060500u) & 0xffffu;
+            const uint32_t v = (s[(c + 2) & 3] & 0x00ff0000u) | (s[(c + 3) & 3] & 0xff000000u);
+            t[c] = sub_word(w | v);
+        }
+#pragma unroll
+        for (int c = 0; c < 4; ++c) s[c] = (r < NR ? mix_word(t[c]) : t[c]) ^ rk[4 * r + c];
+    }
+    return make_uint4(s[0], s[1], s[2], s[3]);
+}
+
+__device__ __forceinline__ uint32_t wave_max(uint32_t v) {
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) {
+        const uint32_t o = (uint32_t)__shfl_xor((int)v, off, 64);
+        v = o > v ? o : v;
+    }
+    return __builtin_amdgcn_readfirstlane(v);
+}
+
+// The chunk loop.  HOOKED (every record of the wave 16-byte aligned): the
+// GHASH of chunk j-1 runs inside chunk j's middle AES rounds, GH blocks per
+// round, so that its serial chain of table lookups hides behind the S-box
+// gates of both waves of the SIMD.  Its input (the ciphertext just stored for
+// seal, the input for open) is re-read from memory one round ahead straight
+// into a per-wave LDS staging buffer (global_load_lds_dwordx4: no VGPRs held
+// across the round); out-of-range blocks read a harmless address and leave y
+// unchanged, so the round stays one basic block.  The last chunk's blocks are
+// hashed after the loop.  Not HOOKED: GHASH block by block after the XOR.
+template <int NR, bool OPEN, bool HOOKED>
+__device__ __forceinline__ uint4 gcm_bs_chunks(const bs::BsKeyMasks& km, const uint32_t* rk,
+                                               const uint32_t* s1w, uint4 rkl, const uint8_t* in,
+                                               uint8_t* out, uint32_t nfull, uint32_t nch,
+                                               uint32_t stage, const uint8_t* safe, uint4 y,
+                                               bool valid) {
+    // fewest full blocks over the wave's valid lanes (wave-uniform)
+    uint32_t nmin = valid ? nfull : 0xffffffffu;
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) {
+        const uint32_t o = (uint32_t)__shfl_xor((int)nmin, off, 64);
+        nmin = o < nmin ? o : nmin;
+    }
+    nmin = __builtin_amdgcn_readfirstlane(nmin);
+    constexpr int GH = (32 + NR - 3) / (NR - 2);   // 4 for AES-128, 3 for AES-256
+    const uint8_t* ghsrc = OPEN ? in : out;
+    const uint32_t lane16 = (threadIdx.x & 63u) << 4;
+    typedef __attribute__((address_space(1))) void gvoid;
+    typedef __attribute__((address_space(3))) void lvoid;
+    for (uint32_t j = 0; j < nch; ++j) {
+        const uint32_t g0 = 32u * (j - 1), glim = nfull < 32u * j ? nfull : 32u * j;
+        // stage round r's GH blocks (of chunk j-1) into buffer r & 1 (for
+        // r = NR, a harmless reload of block 0's slot address)
+        auto prefetch = [&](int r) {
+#pragma unroll
+            for (int u = 0; u < GH; ++u) {
+                const uint32_t gb = g0 + GH * (r - 2) + u;
+                const uint8_t* p = (j != 0 && gb < glim) ? ghsrc + 16 * gb : safe;
+                __builtin_amdgcn_global_load_lds((gvoid*)p,
+                                                 (lvoid*)(uintptr_t)(stage + ((r & 1) * 4 + u) * 1024),
+                                                 16, 0, 0);
+            }
+        };
+        // one GHASH block per four S-box steps, four table rows in flight at
+        // a time (16 VGPRs): step 4u: read block u from the staging buffer,
+        // x = y ^ c, issue rows 0-3; steps 4u+1..4u+3: fold the rows in
+        // flight, issue the next four; the fold of rows 12-15 (at the next
+        // block's first step, or after the last S-box) yields y.  A select
+        // keeps y for blocks outside the previous chunk / the record.
+        uint4 x = make_uint4(0, 0, 0, 0), z = make_uint4(0, 0, 0, 0);
+        uint4 e[4], c[GH];
+        auto rows = [&](int g) {   // table rows 4g .. 4g+3: byte positions of word g
+            const uint32_t v = g == 0 ? x.x : g == 1 ? x.y : g == 2 ? x.z : x.w;
+            e[0] = lds_u128(((v << 4) & 0xff0u) + 4096 * (4 * g + 0));
+            e[1] = lds_u128(((v >> 4) & 0xff0u) + 4096 * (4 * g + 1));
+            e[2] = lds_u128(((v >> 12) & 0xff0u) + 4096 * (4 * g + 2));
+            e[3] = lds_u128(((v >> 20) & 0xff0u) + 4096 * (4 * g + 3));
+        };
+        auto fold = [&]() {
+            z = xor4_3(z, e[0], e[1]);
+            z = xor4_3(z, e[2], e[3]);
+        };
+        auto finish = [&](int r, int u) {   // rows 12-15 of block u are in flight
+            fold();
+            const bool ok = j != 0 && g0 + GH * (r - 2) + u < glim;
+            y.x = ok ? z.x : y.x;
+            y.y = ok ? z.y : y.y;
+            y.z = ok ? z.z : y.z;
+            y.w = ok ? z.w : y.w;
+        };
+        auto hook = [&](int r, int k) {
+            if (!HOOKED) return;
+            if (k == 0) {
+                // this round's blocks out of staging buffer r & 1 (the DMA of the
+                // previous round), then the next round's DMA into the other one
+#pragma unroll
+                for (int u = 0; u < GH; ++u) c[u] = lds_u128(stage + ((r & 1) * 4 + u) * 1024 + lane16);
+                prefetch(r + 1);
+            }
+#pragma unroll
+            for (int u = 0; u < GH; ++u) {
+                if (k == 4 * u) {
+                    if (u) finish(r, u - 1);
+                    x = xor4(y, c[u]);
+                    z = make_uint4(0, 0, 0, 0);
+                    rows(0);
+                } else if (k == 4 * u + 1 || k == 4 * u + 2 || k == 4 * u + 3) {
+                    fold();
+                    rows(k - 4 * u);
+                }
+            }
+            if (k == 15) finish(r, GH - 1);
+        };
+        if (HOOKED) {
+            __builtin_amdgcn_s_waitcnt(0);   // chunk j-1's stores are done before they are re-read
+            prefetch(2);
+        }
+        uint32_t w[4][32];
+        bs::ctr32<NR, 0, bs::BsKeyMasks, 1, HOOKED>(km, rk[3], s1w, 2u + 32u * j, w, hook);
+        auto xor_ks = [&](uint4 d, int q) {
+            return make_uint4(xor3(d.x, w[0][q], rkl.x), xor3(d.y, w[1][q], rkl.y),
+                              xor3(d.z, w[2][q], rkl.z), xor3(d.w, w[3][q], rkl.w));
+        };
+        if (HOOKED && 32u * j + 32u <= nmin) {
+            // Every valid lane of the wave has all 32 blocks.  Loads run one
+            // batch of 8 ahead of the XOR/stores and are issued before the
+            // transposes they wait behind: the vector memory counter is in
+            // order over loads AND stores, so a load issued after a store
+            // would also wait for that store.
+            if (valid) {
+                const uint8_t* ip = in + 512u * j;
+                uint8_t* op = out + 512u * j;
+                constexpr int B = 4;   // blocks per batch; two batches in flight
+                uint4 dv[2][B];
+                auto ld = [&](int bt) {
+#pragma unroll
+                    for (int t = 0; t < B; ++t)
+                        dv[bt & 1][t] = *reinterpret_cast<const uint4*>(ip + 16 * (B * bt + t));
+                };
+                auto st = [&](int bt) {
+#pragma unroll
+                    for (int t = 0; t < B; ++t)
+                        *reinterpret_cast<uint4*>(op + 16 * (B * bt + t)) = xor_ks(dv[bt & 1][t], B * bt + t);
+                };
+                auto tr = [&](int h) {
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) bs::transpose32_half(w[q], h);
+                };
+#define TG_SB __builtin_amdgcn_sched_barrier(0)
+                ld(0); TG_SB; ld(1); TG_SB; tr(0); TG_SB;
+#pragma unroll
+                for (int bt = 0; bt < 32 / B; ++bt) {
+                    st(bt); TG_SB;
+                    if (bt + 2 < 32 / B) { ld(bt + 2); TG_SB; }
+                    if (B * (bt + 2) == 16) { tr(1); TG_SB; }
+                }
+#undef TG_SB
+            }
+            continue;
+        }
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int q = 0; q < 4; ++q) bs::transpose32_half(w[q], h);
+            __builtin_amdgcn_sched_barrier(0);
+            auto block = [&](int q) {
+                const uint32_t blk = 32u * j + q;
+                const uint4 d = load16(in + 16 * blk, HOOKED);
+                const uint4 c = xor_ks(d, q);
+                store16(out + 16 * blk, c, HOOKED);
+                if (!HOOKED) y = gmul_lowreg(xor4(y, OPEN ? d : c));
+            };
+            if (32u * j + 16u * h + 16u <= nmin) {
+                // every valid lane of the wave has these 16 blocks: one basic
+                // block, so the loads are issued together, not one latency each
+                if (valid) {
+#pragma unroll
+                    for (int q = 16 * h; q < 16 * h + 16; ++q) block(q);
+                }
+            } else {
+#pragma unroll
+                for (int q = 16 * h; q < 16 * h + 16; ++q)
+                    if (32u * j + q < nfull) block(q);
+            }
+        }
+    }
+    // HOOKED: GHASH of the last chunk's blocks (stored above; reread in order)
+    if (HOOKED && nch) {
+        // the cipher state is dead here: load the (up to 32) blocks first,
+        // eight at a time, so only the multiply chain is serial
+        for (uint32_t b0 = 32u * (nch - 1); b0 < nfull; b0 += 8) {
+            uint4 cb[8];
+#pragma unroll
+            for (int t = 0; t < 8; ++t)
+                cb[t] = b0 + t < nfull ? *reinterpret_cast<const uint4*>(ghsrc + 16 * (b0 + t))
+                                       : make_uint4(0, 0, 0, 0);
+#pragma unroll
+            for (int t = 0; t < 8; ++t)
+                if (b0 + t < nfull) y = gmul(xor4(y, cb[t]));
+        }
+    }
+    return y;
+}
+
+template <int NR, bool OPEN>
+__global__ __launch_bounds__(kBsThreads, 1) void gcm_bs_kernel(const GcmKeyDev* __restrict__ key,
+                                                              tg_batch b) {
+    uint4* lds = g_lds;
+    for (int e = threadIdx.x; e < kGhashEntries; e += blockDim.x) lds[e] = key->ghash[e];
+    if (threadIdx.x < 64) {   // S(x) = byte 1 of Te0[x]
+        uint32_t v = 0;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) v |= ((c_te.te0[4 * threadIdx.x + q] >> 8) & 0xffu) << (8 * q);
+        reinterpret_cast<uint32_t*>(lds)[kSboxBase / 4 + threadIdx.x] = v;
+    }
+    __syncthreads();
+
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const bool valid = i < b.n;
+    const uint32_t* rk = key->rk;
+    const uint32_t len = valid ? rec_len(b, i) : 0u;
+    const uint32_t nfull = len >> 4, tail = len & 15;
+    const uint32_t nch = wave_max((nfull + 31) >> 5);
+    const uint8_t* in = valid ? rec_in(b, i) : nullptr;
+    uint8_t* out = valid ? rec_out(b, i) : nullptr;
+    const bool aligned = (((uintptr_t)in | (uintptr_t)out) & 15) == 0;
+
+    uint4 nv = make_uint4(0, 0, 0, 0);
+    if (valid) nv = load_partial(b.nonce + 12 * i, 12);
+    // first-round S-box of the nonce bytes, without the 0x63 (see aes_bs.h)
+    const uint32_t s1w[3] = {sub_word(nv.x ^ rk[0]) ^ 0x63636363u, sub_word(nv.y ^ rk[1]) ^ 0x63636363u,
+                             sub_word(nv.z ^ rk[2]) ^ 0x63636363u};
+    const uint4 rkl = make_uint4(rk[4 * NR] ^ 0x63636363u, rk[4 * NR + 1] ^ 0x63636363u,
+                                 rk[4 * NR + 2] ^ 0x63636363u, rk[4 * NR + 3] ^ 0x63636363u);
+
+    // GHASH over the AAD, zero-padded (aesgcm.py:69-79)
+    uint4 y = make_uint4(0, 0, 0, 0);
+    if (valid) {
+        const uint8_t* ad = rec_aad(b, i);
+        const uint32_t alen = rec_aad_len(b, i);
+        for (uint32_t off = 0; off < alen; off += 16) {
+            const uint32_t m = alen - off < 16 ? alen - off : 16;
+            y = gmul_lowreg(xor4(y, load_partial(ad + off, m)));
+        }
+    }
+
+    // CTR from nonce || be32(2) (aesgcm.py:118-120), GHASH over the ciphertext
+    // (aesgcm.py:69-79).
+    const bs::BsKeyMasks km{key->bsmask};
+    const uint32_t stage = kStageBase + (threadIdx.x >> 6) * kStageWave;
+    if (__all(aligned))
+        y = gcm_bs_chunks<NR, OPEN, true>(km, rk, s1w, rkl, in, out, nfull, nch, stage,
+                                          reinterpret_cast<const uint8_t*>(key->ghash), y, valid);
+    else
+        y = gcm_bs_chunks<NR, OPEN, false>(km, rk, s1w, rkl, in, out, nfull, nch, stage,
+                                           reinterpret_cast<const uint8_t*>(key->ghash), y, valid);
+    if (!valid) return;
+    if (tail) {
+        const uint4 ks = aes_block_sb<NR>(rk, make_uint4(nv.x, nv.y, nv.z, bswap32(2u + nfull)));
+        const uint4 d = load_partial(in + 16 * nfull, tail);
+        const uint4 c = mask_tail(xor4(d, ks), tail);
+        store_partial(out + 16 * nfull, c, tail);
+        y = gmul_lowreg(xor4(y, OPEN ? d : c));
+    }
+    // length block: be64(8*alen) || be64(8*len) (aesgcm.py:64)
+    const uint64_t abits = (uint64_t)rec_aad_len(b, i) << 3, cbits = (uint64_t)len << 3;
+    y = gmul_lowreg(xor4(y, make_uint4(bswap32((uint32_t)(abits >> 32)), bswap32((uint32_t)abits),
+                                bswap32((uint32_t)(cbits >> 32)), bswap32((uint32_t)cbits))));
+    // J0 = nonce || be32(1): the tag mask (aesgcm.py:112-115)
+    const uint4 tag = xor4(y, aes_block_sb<NR>(rk, make_uint4(nv.x, nv.y, nv.z, bswap32(1u))));
+    if (!OPEN) {
+        store16(out + len, tag, aligned && tail == 0);
+        return;
+    }
+    // open: compare before releasing (aesgcm.py:148-149, constanttime.py:209-218)
+    const uint4 exp = load16(in + len, aligned && tail == 0);
+    const uint32_t diff = (exp.x ^ tag.x) | (exp.y ^ tag.y) | (exp.z ^ tag.z) | (exp.w ^ tag.w);
+    if (b.status) b.status[i] = diff == 0;
+    if (diff) {
+        const uint4 z = make_uint4(0, 0, 0, 0);
+        for (uint32_t k = 0; k < nfull; ++k) store16(out + 16 * k, z, aligned);
+        if (tail) store_partial(out + 16 * nfull, z, tail);
+    }
+}
+
+template <int NR, bool OPEN>
+int launch_bs(const GcmKeyDev* key, const tg_batch& b, hipStream_t s) {
+    static bool attr_set = false;
+    if (!attr_set) {
+        if (hipFuncSetAttribute((const void*)gcm_bs_kernel<NR, OPEN>,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)kBsLds) != hipSuccess)
+            return TG_EHIP;
+        attr_set = true;
+    }
+    const uint64_t blocks = (b.n + kBsThreads - 1) / kBsThreads;
+    hipLaunchKernelGGL((gcm_bs_kernel<NR, OPEN>), dim3((unsigned)blocks), dim3(kBsThreads), kBsLds, s,
+                       key, b);
+    return hipGetLastError() == hipSuccess ? TG_OK : TG_EHIP;
+}
+
 // Key-table kernel (many sessions per batch, BASELINE config 4): lane i uses
 // key key_idx[i]; its round keys are staged into a private LDS row (272-byte
 // stride: conflict-free ds_read_b128) and GHASH is the table-free multiply.
@@ -422,16 +799,14 @@ int launch_v(const GcmKeyDev* key, const tg_batch& b, hipStream_t s) {
     return hipGetLastError() == hipSuccess ? TG_OK : TG_EHIP;
 }
 
-// Tuning variants (TLSGPU_GCM_VARIANT, for measurement only): blocks per lane
-// iteration G x threads per workgroup x GHASH flavour.  Default: G = 4, 1024
-// threads, 8-bit tables (fastest measured; profiles/r01/gcm_variant_sweep.txt).
+// Kernel choice (TLSGPU_GCM_VARIANT, read per launch, for tests and measurement):
+//   0 / unset  T-table kernel, G = 4, 1024 threads, 8-bit GHASH tables (fastest
+//              measured: profiles/r01/gcm_variant_sweep.txt, bitsliced_gcm.txt);
+//   1..3       T-table tuning variants;
+//   4          the bitsliced kernel (gcm_bs_kernel).
 int variant() {
-    static int v = -1;
-    if (v < 0) {
-        const char* e = getenv("TLSGPU_GCM_VARIANT");
-        v = e ? atoi(e) : 0;
-    }
-    return v;
+    const char* e = getenv("TLSGPU_GCM_VARIANT");
+    return e ? atoi(e) : 0;
 }
 
 template <int NR, bool OPEN>
@@ -440,6 +815,7 @@ int launch(const GcmKeyDev* key, const tg_batch& b, hipStream_t s) {
         case 1: return launch_v<NR, OPEN, 2, 1024, 0>(key, b, s);
         case 2: return launch_v<NR, OPEN, 2, 1024, 2>(key, b, s);
         case 3: return launch_v<NR, OPEN, 2, 512, 1>(key, b, s);
+        case 4: return launch_bs<NR, OPEN>(key, b, s);
         default: return launch_v<NR, OPEN, 4, 1024, 0>(key, b, s);
     }
 }

@@ -513,6 +513,7 @@ int tg_key_create(int alg, const uint8_t* keys, size_t keylen, size_t nkeys, tg_
             uint8_t zero[16] = {0}, h[16];
             aes.encrypt(rk, nr, zero, h);                     // H = E_K(0^128)
             build_ghash_tables(h, hk->ghash);
+            for (int e = 0; e < 128 * (nr + 1); ++e) hk->bsmask[e] = tg::bs_mask_word(hk->rk, e);
             e = hipMalloc(&k->dev_key, sizeof(tg::GcmKeyDev));
             if (e == hipSuccess) e = hipMemcpy(k->dev_key, hk, sizeof(tg::GcmKeyDev), hipMemcpyHostToDevice);
             if (e != hipSuccess) rc = fail(TG_EHIP, "key upload: %s", hipGetErrorString(e));

@@ -22,7 +22,17 @@ struct GcmKeyDev {
     uint32_t rounds;       // 10 (AES-128) or 14 (AES-256)
     uint32_t pad[3];
     uint4 ghash[kGhashEntries];
+    // bitsliced AES (aes_bs.h BsKeyMasks): plane mask (r, k, b) at (16 r + k) 8 + b
+    // = 0 or ~0 by bit b of byte k of rk_r ^ (r ? 0x63 : 0) (see bs_mask_word)
+    uint32_t bsmask[15 * 128];
 };
+
+// Entry e of GcmKeyDev::bsmask from the round-key words.
+__host__ __device__ inline uint32_t bs_mask_word(const uint32_t* rk, int e) {
+    const int r = e >> 7, k = (e >> 3) & 15, bit = e & 7;
+    const uint32_t w = rk[4 * r + (k >> 2)] ^ (r ? 0x63636363u : 0u);
+    return ((w >> (8 * (k & 3) + bit)) & 1u) ? 0xffffffffu : 0u;
+}
 
 // One entry of an AES-GCM key table (many sessions in one batch): the round
 // keys and H = E_K(0) in normal polynomial order (see GhashClmul).

@@ -357,6 +357,12 @@ __global__ void ghash_table_kernel(GcmKeyDev* key) {
     key->ghash[e] = make_uint4(w[0], w[1], w[2], w[3]);
 }
 
+// GcmKeyDev::bsmask from the round keys (after aes_setup_kernel, layout 0).
+__global__ void bs_mask_kernel(GcmKeyDev* key) {
+    const int e = blockIdx.x * blockDim.x + threadIdx.x;
+    if (e < 128 * (int)(key->rounds + 1)) key->bsmask[e] = bs_mask_word(key->rk, e);
+}
+
 }  // namespace
 }  // namespace tg
 
@@ -396,6 +402,8 @@ int tg_launch_aes_setup(int keylen, int layout, const uint8_t* keys, uint64_t n,
     if (layout == 0) {
         tg::GcmKeyDev* k = static_cast<tg::GcmKeyDev*>(out);
         hipLaunchKernelGGL(tg::ghash_table_kernel, dim3(tg::kGhashEntries / 256), dim3(256), 0, s, k);
+        if (hipGetLastError() != hipSuccess) return TG_EHIP;
+        hipLaunchKernelGGL(tg::bs_mask_kernel, dim3(15 * 128 / 256), dim3(256), 0, s, k);
         if (hipGetLastError() != hipSuccess) return TG_EHIP;
         if (hipMemsetAsync(&k->ghash[0], 0, sizeof(uint4), s) != hipSuccess) return TG_EHIP;
     }
