@@ -98,11 +98,17 @@ def main():
                          "WRITE_SIZE passes at this config) for roofline.traffic")
     ap.add_argument("--record-align", type=int, default=128,
                     help="byte alignment of each sealed record (ct||tag) in the packed batch")
-    ap.add_argument("--config", default="headline", choices=["headline", "c4", "c5"],
+    ap.add_argument("--config", default="headline", choices=["headline", "c4", "c5", "ingest"],
                     help="headline = BASELINE configs[1]+[2] (the metric); c4 = configs[3] "
                          "(AES-256-GCM, 65536 keys, Zipf lengths); c5 = configs[4] (TLS 1.3 "
-                         "AES-128-GCM seal, 16385-byte inner plaintext, seq-sharded)")
+                         "AES-128-GCM seal, 16385-byte inner plaintext, seq-sharded); ingest = "
+                         "the host ingest pipeline (tlsgpu.ingest, SURVEY 8(f) row 3), host "
+                         "memory to host memory")
+    ap.add_argument("--ingest-mib", type=int, default=2048,
+                    help="application data per direction for --config ingest")
     args = ap.parse_args()
+    if args.config == "ingest":
+        return run_ingest(args)
     if args.config == "c4":
         return run_config4(args)
     if args.config == "c5":
@@ -397,6 +403,83 @@ def run_config4(args):
     print(json.dumps(line), flush=True)
     if not ok:
         sys.exit(3)
+
+
+class _NullSink(object):
+    """A socket stand-in that takes the wire bytes without copying them."""
+
+    def __init__(self):
+        self.bytes = 0
+
+    def sendall(self, mv):
+        self.bytes += len(mv)
+
+
+class _MemSink(object):
+    def __init__(self):
+        self.parts = []
+
+    def sendall(self, mv):
+        self.parts.append(bytes(mv))
+
+
+def run_ingest(args):
+    """Host ingest pipeline (tlsgpu.ingest): application data in host memory
+    -> RecordWriter (pinned slots, H2D, device framing + AEAD, device pack,
+    D2H) -> wire bytes; and wire bytes -> RecordReader (header scan, H2D,
+    device spread + open, D2H) -> application data.  TLS 1.3, 16 KiB records.
+    Reported in DESIGN.md (end-to-end row), never as the headline value."""
+    import hashlib
+    import numpy as np
+    import torch
+    import tlsgpu
+    torch.cuda.set_device(0)
+    total = args.ingest_mib << 20
+    blk = np.random.default_rng(0x7718).integers(0, 256, 64 << 20, dtype=np.uint8).tobytes()
+    data = blk * (total // len(blk))
+    want = hashlib.sha256(data).hexdigest()
+    iv = bytes(range(12))
+    res = {}
+    for alg, obj in (("aes128gcm", lambda: tlsgpu.HipAESGCM(bytearray(16))),
+                     ("chacha20-poly1305", lambda: tlsgpu.HipCHACHA20_POLY1305(bytearray(32)))):
+        mv = memoryview(data)
+        # warm-up: build the wire stream once (also the reader's input)
+        ms = _MemSink()
+        w = tlsgpu.RecordWriter(ms, obj(), tlsgpu.TLS13, iv, batch_records=8192)
+        for p in range(0, len(data), 64 << 20):
+            w.write(mv[p:p + (64 << 20)])
+        w.flush()
+        wire = b"".join(ms.parts)
+        del ms
+        ns = _NullSink()
+        w = tlsgpu.RecordWriter(ns, obj(), tlsgpu.TLS13, iv, batch_records=8192)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for p in range(0, len(data), 64 << 20):
+            w.write(mv[p:p + (64 << 20)])
+        w.flush()
+        t_w = time.perf_counter() - t0
+        r = tlsgpu.RecordReader(obj(), tlsgpu.TLS13, iv, batch_records=8192,
+                                buffer_bytes=160 << 20)
+        wv = memoryview(wire)
+        outbuf = np.empty(total, np.uint8)
+        ov, pos = memoryview(outbuf), 0
+        t0 = time.perf_counter()
+        for p in range(0, len(wire), 128 << 20):   # socket reads of 128 MiB
+            r.feed(wv[p:p + (128 << 20)])
+            pos += len(r.read_application_data(out=ov[pos:]))
+        t_r = time.perf_counter() - t0
+        ok = (pos == total and hashlib.sha256(outbuf).hexdigest() == want
+              and ns.bytes == len(wire))
+        res[alg] = {"write_GiBps": round(total / t_w / 2 ** 30, 2),
+                    "read_GiBps": round(total / t_r / 2 ** 30, 2),
+                    "records": w.records_sent, "wire_bytes": len(wire), "verified": ok}
+        del wire, outbuf, ov
+    line = {"metric": "GiB/s host ingest pipeline (RecordWriter / RecordReader), TLS 1.3, "
+                      "16 KiB records, host memory to host memory",
+            "unit": "GiB/s", "n_gpus": 1, "app_data_bytes": total, "dtype": "u8",
+            "data": "synthetic", "per_alg": res}
+    print(json.dumps(line), flush=True)
 
 
 def end_to_end(torch, tlsgpu, ciphers, aad, nonces, L, n):

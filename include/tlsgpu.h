@@ -197,6 +197,28 @@ int tg_hkdf_expand_label(int hashlen, const uint8_t* secrets, uint64_t n, const 
                          uint8_t* out, void* stream);
 int tg_key_create_device(int alg, const uint8_t* keys, size_t keylen, size_t nkeys,
                          tg_key** out, void* stream);
+/* Host ingest pipeline (tlsgpu/ingest.py) -- the
+ * batched counterpart of RecordSocket (recordlayer.py:35-237).
+ * tg_scan_records (HOST memory, no GPU): walk the 5-byte record headers
+ *   (RecordHeader3, RecordSocket._recvHeader :169-205) of the wire bytes
+ *   buf[0, len): record k starts at off[k] and spans rlen[k] = 5 + body bytes.
+ *   Stops at the first incomplete record or after max_n records; *consumed =
+ *   the bytes of the complete records.  Returns the record count, or
+ *   TG_EOVERFLOW if a header declares body > max_body (TLSRecordOverflow,
+ *   RecordSocket.recv :225-229: recv_record_limit + 2048, TLS 1.3 + 256) and
+ *   TG_EHEADER for a first byte that is no TLS content type (20..24; the
+ *   reference would try SSLv2 framing there).  Records before the bad header
+ *   are reported through *consumed and off/rlen (the return value is then
+ *   negative, so count them by *consumed).
+ * tg_gather (DEVICE memory): for i < n copy len[i] bytes from
+ *   src + src_off[i] to dst + dst_off[i] (pack aligned wire records into
+ *   one contiguous stream and back).  off/len arrays in device memory. */
+#define TG_EOVERFLOW (-75)
+#define TG_EHEADER (-71)
+int64_t tg_scan_records(const uint8_t* buf, size_t len, uint32_t max_body, uint64_t* off,
+                        uint32_t* rlen, size_t max_n, size_t* consumed);
+int tg_gather(const uint8_t* src, const uint64_t* src_off, const uint32_t* len, uint8_t* dst,
+              const uint64_t* dst_off, uint64_t n, void* stream);
 /* Device memory helpers so a ctypes host needs no other GPU runtime. */
 int tg_malloc(void** p, size_t bytes);
 int tg_free(void* p);

@@ -1,0 +1,151 @@
+"""GPU: the host ingest pipeline (tlsgpu/ingest.py).
+
+RecordWriter output is compared record by record with the framing oracle
+(oracle/records.py, pinned to the reference RecordLayer's wire bytes); the
+RecordReader gets the wire stream back in socket-sized pieces and must return
+the original fragments, then raise the reference's exceptions for a tampered
+record and an oversized header; a socketpair round trip runs both ends
+concurrently."""
+import random
+import socket
+import threading
+
+import numpy as np
+import pytest
+
+from oracle import records as orec
+from vectors import detbytes
+
+pytestmark = pytest.mark.gpu
+
+SUITES = [("tls13", "aes128gcm", 16, 12), ("tls13", "chacha20-poly1305", 32, 12),
+          ("tls12", "aes256gcm", 32, 4), ("tls12", "chacha20-poly1305", 32, 12),
+          ("tls13", "aes128ccm", 16, 12)]
+
+
+@pytest.fixture(scope="module")
+def torch():
+    import torch as t
+    if not t.cuda.is_available():
+        pytest.fail("GPU tests need a visible MI355X")
+    return t
+
+
+@pytest.fixture(scope="module")
+def tg(torch):
+    import tlsgpu
+    return tlsgpu
+
+
+def _key(tg, alg, key):
+    if alg.startswith("chacha"):
+        return tg.HipCHACHA20_POLY1305(bytearray(key))
+    if "ccm" in alg:
+        return tg.HipAESCCM(bytearray(key))
+    return tg.HipAESGCM(bytearray(key))
+
+
+class Sink(object):
+    def __init__(self):
+        self.buf = bytearray()
+
+    def sendall(self, mv):
+        self.buf += bytes(mv)
+
+
+def _messages(seed):
+    rng = random.Random(seed)
+    sizes = [0, 1, 15, 16, 2 ** 14 - 1, 2 ** 14, 2 ** 14 + 1, 3 * 2 ** 14 + 7, 100000]
+    sizes += [rng.randint(0, 70000) for _ in range(12)]
+    return [detbytes("ingest-%d-%d" % (seed, i), n) for i, n in enumerate(sizes)]
+
+
+def _fragments(msgs, limit):
+    out = []
+    for m in msgs:
+        if not m:
+            out.append(b"")
+        for p in range(0, len(m), limit):
+            out.append(bytes(m[p:p + limit]))
+    return out
+
+
+@pytest.mark.parametrize("ver,alg,klen,ivlen", SUITES)
+def test_writer_vs_oracle_and_reader_roundtrip(torch, tg, ver, alg, klen, ivlen):
+    key = detbytes("ingest-key-" + alg, klen)
+    iv = detbytes("ingest-iv-" + alg, ivlen)
+    version = tg.TLS13 if ver == "tls13" else tg.TLS12
+    pad = 3 if ver == "tls13" else 0
+    sink = Sink()
+    w = tg.RecordWriter(sink, _key(tg, alg, key), version, iv, seq0=5, batch_records=7,
+                        pad=pad)
+    msgs = _messages(klen + ivlen)
+    for m in msgs:
+        w.write(m)
+    w.flush()
+    frags = _fragments(msgs, 2 ** 14)
+    want = b"".join(orec.seal_record(ver, alg, key, iv, 5 + i, 23, f, pad=pad)
+                    for i, f in enumerate(frags))
+    assert w.records_sent == len(frags)
+    assert bytes(sink.buf) == want
+    # reader: the same stream in uneven socket reads
+    r = tg.RecordReader(_key(tg, alg, key), version, iv, seq0=5, batch_records=5)
+    got, rng, pos = [], random.Random(1), 0
+    while pos < len(want):
+        k = rng.choice([1, 5, 100, 4096, 20000, 70000])
+        r.feed(want[pos:pos + k])
+        pos += k
+        got.extend(r.records())
+    assert [t for t, _ in got] == [23] * len(frags)
+    assert [bytes(d) for _, d in got] == frags
+
+
+def test_reader_errors(torch, tg):
+    key, iv = detbytes("ingest-err", 16), detbytes("ingest-err-iv", 12)
+    recs = [orec.seal_record("tls13", "aes128gcm", key, iv, i, 23, detbytes("e%d" % i, 300))
+            for i in range(6)]
+    bad = bytearray(recs[3])
+    bad[-1] ^= 1
+    r = tg.RecordReader(_key(tg, "aesgcm", key), tg.TLS13, iv)
+    r.feed(b"".join(recs[:3]) + bytes(bad) + b"".join(recs[4:]))
+    ok = r.records()
+    assert [bytes(d) for _, d in ok] == [bytes(detbytes("e%d" % i, 300)) for i in range(3)]
+    from tlsgpu.ingest import TLSBadRecordMAC, TLSRecordOverflow
+    with pytest.raises(TLSBadRecordMAC):
+        r.records()
+    r2 = tg.RecordReader(_key(tg, "aesgcm", key), tg.TLS13, iv)
+    r2.feed(recs[0] + bytes([23, 3, 3, 0x41, 0x01]) + bytes(0x4101))   # > 2**14 + 256
+    assert len(r2.records()) == 1
+    with pytest.raises(TLSRecordOverflow):
+        r2.records()
+
+
+def test_socketpair_bulk(torch, tg):
+    """Both ends over a real socket: 64 MiB of application data."""
+    key, iv = detbytes("ingest-sock", 32), detbytes("ingest-sock-iv", 12)
+    a, b = socket.socketpair()
+    data = np.random.default_rng(3).integers(0, 256, 64 << 20, dtype=np.uint8).tobytes()
+    w = tg.RecordWriter(a, _key(tg, "chacha", key), tg.TLS13, iv, batch_records=512)
+
+    def send():
+        for p in range(0, len(data), 1 << 20):
+            w.write(data[p:p + (1 << 20)])
+        w.flush()
+        a.shutdown(socket.SHUT_WR)
+
+    t = threading.Thread(target=send)
+    t.start()
+    r = tg.RecordReader(_key(tg, "chacha", key), tg.TLS13, iv, batch_records=512)
+    out = bytearray()
+    while True:
+        chunk = b.recv(1 << 20)
+        if not chunk:
+            break
+        r.feed(chunk)
+        for ct, d in r.records():
+            assert ct == 23
+            out += d
+    t.join()
+    a.close()
+    b.close()
+    assert out == data

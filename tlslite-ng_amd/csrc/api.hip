@@ -679,6 +679,35 @@ int tg_memcpy_d2h(void* dst, const void* src, size_t bytes, void* stream) {
     return TG_OK;
 }
 
+int64_t tg_scan_records(const uint8_t* buf, size_t len, uint32_t max_body, uint64_t* off,
+                        uint32_t* rlen, size_t max_n, size_t* consumed) {
+    if (!consumed || (len && !buf) || (max_n && (!off || !rlen)))
+        return fail(TG_EINVAL, "null argument");
+    size_t pos = 0, k = 0;
+    *consumed = 0;
+    while (k < max_n && len - pos >= 5) {
+        const uint8_t type = buf[pos];
+        if (type < 20 || type > 24) return fail(TG_EHEADER, "record %zu: content type %u", k, type);
+        const uint32_t body = ((uint32_t)buf[pos + 3] << 8) | buf[pos + 4];
+        if (body > max_body) return fail(TG_EOVERFLOW, "record %zu: %u > %u bytes", k, body, max_body);
+        if (len - pos < 5 + (size_t)body) break;   // incomplete: wait for more bytes
+        off[k] = pos;
+        rlen[k] = 5 + body;
+        pos += 5 + body;
+        *consumed = pos;
+        ++k;
+    }
+    return (int64_t)k;
+}
+
+int tg_gather(const uint8_t* src, const uint64_t* src_off, const uint32_t* len, uint8_t* dst,
+              const uint64_t* dst_off, uint64_t n, void* stream) {
+    if (n && (!src || !src_off || !len || !dst || !dst_off)) return fail(TG_EINVAL, "null argument");
+    if (n == 0) return TG_OK;
+    int rc = tg_launch_gather(src, src_off, len, dst, dst_off, n, static_cast<hipStream_t>(stream));
+    return rc ? fail(rc, "gather kernel launch failed") : TG_OK;
+}
+
 int tg_stream_sync(void* stream) {
     HIP_TRY(hipStreamSynchronize(static_cast<hipStream_t>(stream)));
     return TG_OK;

@@ -161,5 +161,7 @@ int tg_launch_hkdf(int hashlen, const tg::HkdfMsg& msg, const uint8_t* secrets, 
                    uint8_t* out, hipStream_t s);
 int tg_launch_aes_setup(int keylen, int layout, const uint8_t* keys, uint64_t n, void* out,
                         hipStream_t s);
+int tg_launch_gather(const uint8_t* src, const uint64_t* src_off, const uint32_t* len, uint8_t* dst,
+                     const uint64_t* dst_off, uint64_t n, hipStream_t s);
 int tg_launch_nonces(int mode, const uint8_t* iv_host, uint64_t seq0, uint64_t n, uint8_t* out,
                      hipStream_t s);

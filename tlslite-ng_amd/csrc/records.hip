@@ -165,6 +165,30 @@ __global__ void open_finish(tg_records r, RecScratch s) {
     r.status[i] = st;
 }
 
+// tg_gather: one workgroup per range; 16-byte vector copies when source and
+// destination are co-aligned, otherwise bytes.  Coalesced: consecutive
+// threads move consecutive 16-byte pieces of the range.
+__global__ void gather_kernel(const uint8_t* __restrict__ src, const uint64_t* __restrict__ src_off,
+                              const uint32_t* __restrict__ len, uint8_t* __restrict__ dst,
+                              const uint64_t* __restrict__ dst_off) {
+    const uint64_t i = blockIdx.x;
+    const uint8_t* s = src + src_off[i];
+    uint8_t* d = dst + dst_off[i];
+    const uint32_t L = len[i];
+    const uint32_t mis = (uint32_t)((uintptr_t)s & 15u);
+    if (mis == ((uintptr_t)d & 15u)) {
+        const uint32_t head = mis ? (16u - mis < L ? 16u - mis : L) : 0u;
+        for (uint32_t k = threadIdx.x; k < head; k += blockDim.x) d[k] = s[k];
+        const uint32_t nvec = (L - head) >> 4;
+        const uint4* sv = reinterpret_cast<const uint4*>(s + head);
+        uint4* dv = reinterpret_cast<uint4*>(d + head);
+        for (uint32_t k = threadIdx.x; k < nvec; k += blockDim.x) dv[k] = sv[k];
+        for (uint32_t k = head + 16u * nvec + threadIdx.x; k < L; k += blockDim.x) d[k] = s[k];
+    } else {
+        for (uint32_t k = threadIdx.x; k < L; k += blockDim.x) d[k] = s[k];
+    }
+}
+
 }  // namespace
 }  // namespace tg
 
@@ -184,4 +208,15 @@ int tg_launch_records_finish(const tg_records& r, const tg::RecScratch& s, hipSt
     const uint64_t blocks = (r.n + tg::kRecThreads - 1) / tg::kRecThreads;
     hipLaunchKernelGGL(tg::open_finish, dim3((unsigned)blocks), dim3(tg::kRecThreads), 0, st, r, s);
     return hipGetLastError() == hipSuccess ? TG_OK : TG_EHIP;
+}
+
+int tg_launch_gather(const uint8_t* src, const uint64_t* src_off, const uint32_t* len, uint8_t* dst,
+                     const uint64_t* dst_off, uint64_t n, hipStream_t s) {
+    for (uint64_t i0 = 0; i0 < n; i0 += 0x7fffffffull) {   // grid.x limit
+        const uint64_t k = n - i0 < 0x7fffffffull ? n - i0 : 0x7fffffffull;
+        hipLaunchKernelGGL(tg::gather_kernel, dim3((unsigned)k), dim3(256), 0, s, src, src_off + i0,
+                           len + i0, dst, dst_off + i0);
+        if (hipGetLastError() != hipSuccess) return TG_EHIP;
+    }
+    return TG_OK;
 }

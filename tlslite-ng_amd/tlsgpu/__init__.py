@@ -13,5 +13,6 @@ from .cipherfactory import (CIPHER_IMPLEMENTATIONS, createAESCCM, createAESCCM_8
                             createAESGCM, createCHACHA20)
 from .records import TLS12, TLS13, open_records, seal_records  # noqa: F401
 from . import keysetup  # noqa: F401
+from .ingest import RecordReader, RecordWriter  # noqa: F401
 
 __version__ = "0.1.0"

@@ -17,6 +17,8 @@ TG_ENONCE = -3
 TG_ENOMEM = -12
 TG_EHIP = -5
 TG_ENODEV = -19
+TG_EOVERFLOW = -75
+TG_EHEADER = -71
 
 TG_AES_GCM = 0
 TG_CHACHA20_POLY1305 = 1
@@ -28,7 +30,7 @@ EXPORTS = ("tg_version", "tg_last_error", "tg_device_count", "tg_init", "tg_key_
            "tg_key_destroy", "tg_key_info", "tg_key_taglen", "tg_seal", "tg_open", "tg_seal_batch",
            "tg_open_batch", "tg_make_nonces", "tg_malloc", "tg_free", "tg_memcpy_h2d",
            "tg_memcpy_d2h", "tg_stream_sync", "tg_seal_records", "tg_open_records",
-           "tg_hkdf_expand_label", "tg_key_create_device")
+           "tg_hkdf_expand_label", "tg_key_create_device", "tg_scan_records", "tg_gather")
 
 TG_TLS12 = 0x0303
 TG_TLS13 = 0x0304
@@ -125,9 +127,12 @@ def load():
     l.tg_memcpy_h2d.argtypes = [p, p, sz, p]
     l.tg_memcpy_d2h.argtypes = [p, p, sz, p]
     l.tg_stream_sync.argtypes = [p]
+    l.tg_scan_records.argtypes = [p, sz, ctypes.c_uint32, p, p, sz, ctypes.POINTER(sz)]
+    l.tg_gather.argtypes = [p, p, p, p, p, u64, p]
     for name in EXPORTS:
         if name not in ("tg_version", "tg_last_error"):
             getattr(l, name).restype = ctypes.c_int
+    l.tg_scan_records.restype = ctypes.c_int64
     _lib = l
     return l
 

@@ -1,0 +1,477 @@
+"""Host ingest pipeline: the batched counterpart of
+RecordSocket (tlslite/recordlayer.py:35-237) around the device framing of
+records.py, for the bulk data of one connection direction.
+
+* ``RecordWriter`` -- RecordLayer.sendRecord (:606-617) + _encryptThenSeal
+  (:536-565) + RecordSocket.send (:83-104) for a stream of records: the
+  application data is fragmented into records of at most ``send_record_limit``
+  bytes (RecordLayer.send_record_limit, :316), copied into a pinned host slot,
+  sealed on the GPU (tg_seal_records: header, TLS 1.2 explicit nonce, TLS 1.3
+  inner type + padding, AEAD), packed into one contiguous wire stream on the
+  device (tg_gather) and copied back to a pinned buffer that goes to the sink's
+  ``sendall``.
+* ``RecordReader`` -- RecordSocket.recv (:207-237) + RecordLayer.recvRecord /
+  _decryptAndUnseal (:780-824) / _tls13_de_pad (:863-884): wire bytes are
+  accumulated in a pinned buffer, the complete records are found by
+  tg_scan_records (host C, with RecordSocket's length limits), copied to the
+  device in one piece, spread into 16-byte aligned slots (tg_gather), opened
+  (tg_open_records) and returned in order as ``(content_type, bytearray)``;
+  the first failing record raises the reference's exception.
+
+Each direction keeps ``nslots`` (default 2) slots, each with its own HIP
+stream: while one batch runs host->device copy, kernels and device->host copy,
+the host fills the next slot (writer) or hands the previous batch's records
+to the caller (reader).  Sequence numbers run on from ``seq0`` as in
+ConnectionState.getSeqNumBytes (:251-256).
+"""
+import ctypes
+
+import numpy as np
+
+from . import _lib
+from .batch import _ptr
+from .records import TLS12, TLS13, open_records, seal_records
+
+
+class TLSProtocolException(Exception):
+    """tlslite.errors.TLSProtocolException (errors.py:195)."""
+
+
+class TLSIllegalParameterException(TLSProtocolException):
+    """errors.py:201"""
+
+
+class TLSUnexpectedMessage(TLSProtocolException):
+    """errors.py:213"""
+
+
+class TLSRecordOverflow(TLSProtocolException):
+    """errors.py:222"""
+
+
+class TLSBadRecordMAC(TLSProtocolException):
+    """errors.py:234"""
+
+
+# tg_open_records status -> the exception _decryptAndUnseal / _tls13_de_pad raise
+_STATUS_EXC = {
+    1: (TLSBadRecordMAC, "Invalid tag, decryption failure"),
+    2: (TLSBadRecordMAC, "Truncated tag"),
+    3: (TLSBadRecordMAC, "Length mismatch"),
+    4: (TLSUnexpectedMessage, "Invalid ContentType for encrypted record"),
+    5: (TLSIllegalParameterException, "Unexpected version in encrypted record"),
+    6: (TLSUnexpectedMessage, "Malformed record layer inner plaintext - content type missing"),
+}
+
+APPLICATION_DATA = 23
+
+
+def _ru(x, m):
+    return (x + m - 1) // m * m
+
+
+def _explicit_nonce(version, key):
+    # TLS 1.2 AES-GCM / AES-CCM carry an 8-byte explicit nonce ("aes" in name)
+    return 8 if version == TLS12 and "aes" in key.name else 0
+
+
+class _Slot(object):
+    """Pinned host + device buffers and a stream for one batch in flight."""
+
+    def __init__(self, torch, nrec, data_stride, wire_stride, wire_lead):
+        self.stream = torch.cuda.Stream()
+        self.event = torch.cuda.Event()
+        self.busy = False
+        u8 = torch.uint8
+        self.h_data = torch.empty(nrec * data_stride, dtype=u8).pin_memory()
+        self.h_wire = torch.empty(nrec * wire_stride, dtype=u8).pin_memory()
+        self.d_data = torch.empty(nrec * data_stride, dtype=u8, device="cuda")
+        self.d_wire = torch.empty(nrec * wire_stride + 16, dtype=u8, device="cuda")
+        self.d_pack = torch.empty(nrec * wire_stride, dtype=u8, device="cuda")
+        # per-record metadata: host staging (pinned) and device copies
+        self.h_len = torch.empty(nrec, dtype=torch.int32).pin_memory()
+        self.h_ctype = torch.empty(nrec, dtype=u8).pin_memory()
+        self.h_pack = torch.empty(nrec, dtype=torch.int64).pin_memory()
+        self.h_status = torch.empty(nrec, dtype=u8).pin_memory()
+        self.d_len = torch.empty(nrec, dtype=torch.int32, device="cuda")
+        self.d_wlen = torch.empty(nrec, dtype=torch.int32, device="cuda")
+        self.d_ctype = torch.empty(nrec, dtype=u8, device="cuda")
+        self.d_pack_off = torch.empty(nrec, dtype=torch.int64, device="cuda")
+        self.d_status = torch.empty(nrec, dtype=u8, device="cuda")
+        idx = torch.arange(nrec, dtype=torch.int64, device="cuda")
+        self.d_data_off = idx * data_stride
+        self.d_wire_off = idx * wire_stride + wire_lead
+        self.n = 0
+        self.nbytes = 0
+
+
+class RecordWriter(object):
+    """Seal and send a stream of records of one connection direction.
+
+    :param sink: object with ``sendall(buffer)`` (a socket, or any byte sink)
+    :param key: the direction's AEAD object (HipAESGCM / HipAESCCM /
+        HipCHACHA20_POLY1305, i.e. ConnectionState.encContext)
+    :param version: TLS12 or TLS13 (records.py)
+    :param fixed_iv: ConnectionState.fixedNonce (12 bytes, or 4 for TLS 1.2
+        AES-GCM / AES-CCM)
+    """
+
+    def __init__(self, sink, key, version, fixed_iv, seq0=0, send_record_limit=2 ** 14,
+                 batch_records=1024, nslots=2, pad=0):
+        import torch
+        if version not in (TLS12, TLS13):
+            raise ValueError("version must be TLS12 or TLS13")
+        self.torch = torch
+        self.sink = sink
+        self.key = key
+        self.version = version
+        self.fixed_iv = bytes(fixed_iv)
+        self.seq = int(seq0)
+        self.limit = int(send_record_limit)
+        self.pad = int(pad) if version == TLS13 else 0
+        self.batch = int(batch_records)
+        self.hdr = 5 + _explicit_nonce(version, key)
+        self.tag = key.tagLength
+        inner = self.limit + (1 + self.pad if version == TLS13 else 0)
+        self.data_stride = _ru(inner + 16, 16)
+        # payload after header (+ explicit nonce) starts 16-byte aligned
+        self.lead = _ru(self.hdr, 16) - self.hdr
+        self.wire_stride = _ru(self.lead + self.hdr + inner + self.tag, 16)
+        self.slots = [_Slot(torch, self.batch, self.data_stride, self.wire_stride, self.lead)
+                      for _ in range(nslots)]
+        self.cur = 0
+        self.records_sent = 0
+        self.bytes_sent = 0
+
+    # -- RecordLayer.sendRecord for application data, batched
+    def write(self, data, content_type=APPLICATION_DATA):
+        """Queue ``data`` as records of at most send_record_limit bytes (an
+        empty ``data`` queues one empty record, as sendRecord does)."""
+        mv = memoryview(bytes(data) if not isinstance(data, (bytes, bytearray, memoryview))
+                        else data).cast("B")
+        src = np.frombuffer(mv, np.uint8)
+        pos = 0
+        while True:
+            s = self.slots[self.cur]
+            if s.busy:
+                self._finish(s)
+            hd = s.h_data.numpy()
+            # whole records: one strided copy for as many as fit in the slot
+            m = min((len(src) - pos) // self.limit, self.batch - s.n)
+            if m > 1:
+                o = s.n * self.data_stride
+                dst = hd[o:o + m * self.data_stride].reshape(m, self.data_stride)
+                dst[:, :self.limit] = src[pos:pos + m * self.limit].reshape(m, self.limit)
+                s.h_len.numpy()[s.n:s.n + m] = self.limit
+                s.h_ctype.numpy()[s.n:s.n + m] = content_type
+                s.n += m
+                pos += m * self.limit
+            else:
+                k = min(len(src) - pos, self.limit)
+                o = s.n * self.data_stride
+                hd[o:o + k] = src[pos:pos + k]
+                s.h_len.numpy()[s.n] = k
+                s.h_ctype.numpy()[s.n] = content_type
+                s.n += 1
+                pos += k
+            if s.n == self.batch:
+                self._launch(s)
+            if pos >= len(src):
+                break
+
+    def flush(self):
+        """Seal what is queued and send everything in order."""
+        s = self.slots[self.cur]
+        if s.n and not s.busy:
+            self._launch(s)
+        for k in range(len(self.slots)):
+            s = self.slots[(self.cur + k) % len(self.slots)]
+            if s.busy:
+                self._finish(s)
+
+    def _wire_len(self, L):
+        inner = L + (1 + self.pad if self.version == TLS13 else 0)
+        return self.hdr + inner + self.tag
+
+    def _launch(self, s):
+        torch = self.torch
+        n = s.n
+        lens = s.h_len.numpy()[:n].astype(np.int64)
+        wl = self._wire_len(lens)
+        pack = s.h_pack.numpy()
+        pack[0] = 0
+        if n > 1:
+            np.cumsum(wl[:-1], out=pack[1:n])
+        s.nbytes = int(wl.sum())
+        pad = None
+        with torch.cuda.stream(s.stream):
+            used = (n - 1) * self.data_stride + int(lens[-1]) if n else 0
+            s.d_data[:used].copy_(s.h_data[:used], non_blocking=True)
+            s.d_len[:n].copy_(s.h_len[:n], non_blocking=True)
+            s.d_ctype[:n].copy_(s.h_ctype[:n], non_blocking=True)
+            s.d_pack_off[:n].copy_(s.h_pack[:n], non_blocking=True)
+            if self.pad:
+                pad = torch.full((n,), self.pad, dtype=torch.int32, device="cuda")
+            seal_records(self.key, self.version, self.fixed_iv, self.seq, n, s.d_data, s.d_data_off,
+                         s.d_len, s.d_ctype, s.d_wire, s.d_wire_off, s.d_wlen, pad_len=pad,
+                         stream=s.stream)
+            gather(s.d_wire, s.d_wire_off, s.d_wlen, s.d_pack, s.d_pack_off, n, stream=s.stream)
+            s.h_wire[:s.nbytes].copy_(s.d_pack[:s.nbytes], non_blocking=True)
+            s.event.record(s.stream)
+        s.keep = pad
+        s.busy = True
+        self.seq += n
+        self.cur = (self.cur + 1) % len(self.slots)
+
+    def _finish(self, s):
+        s.event.synchronize()
+        self.sink.sendall(memoryview(s.h_wire.numpy())[:s.nbytes])
+        self.records_sent += s.n
+        self.bytes_sent += s.nbytes
+        s.n = 0
+        s.busy = False
+
+
+class RecordReader(object):
+    """Receive, check and open a stream of records of one connection
+    direction (wire bytes in, ``(content_type, bytearray)`` out).
+
+    ``feed(wire_bytes)`` queues bytes as they come off the socket;
+    ``records()`` returns the records completed so far, in order.  Errors:
+    TLSRecordOverflow / TLSIllegalParameterException for a bad header
+    (RecordSocket.recv), then per record the exception _decryptAndUnseal or
+    _tls13_de_pad would raise; records before the failing one are returned
+    by ``records()`` first and the error is raised on the next call.
+    """
+
+    def __init__(self, key, version, fixed_iv, seq0=0, recv_record_limit=2 ** 14,
+                 batch_records=1024, buffer_bytes=None):
+        import torch
+        if version not in (TLS12, TLS13):
+            raise ValueError("version must be TLS12 or TLS13")
+        self.torch = torch
+        self.key = key
+        self.version = version
+        self.fixed_iv = bytes(fixed_iv)
+        self.seq = int(seq0)
+        # RecordSocket.recv (:217-222): 2**14 + 2048 always, 2**14 + 256 for TLS 1.3
+        self.max_body = recv_record_limit + (256 if version == TLS13 else 2048)
+        self.batch = int(batch_records)
+        self.hdr = 5 + _explicit_nonce(version, key)
+        self.lead = _ru(self.hdr, 16) - self.hdr
+        self.wire_stride = _ru(self.lead + 5 + self.max_body, 16)
+        self.data_stride = _ru(self.max_body + 16, 16)
+        cap = buffer_bytes or self.batch * (5 + self.max_body)
+        self.h_buf = torch.empty(cap, dtype=torch.uint8).pin_memory()
+        self.fill = 0
+        self.slot = _Slot(torch, self.batch, self.data_stride, self.wire_stride, self.lead)
+        self.h_off = np.empty(self.batch, np.uint64)
+        self.h_rlen = np.empty(self.batch, np.uint32)
+        self.h_plen = torch.empty(self.batch, dtype=torch.int32).pin_memory()
+        self.h_src = torch.empty(self.batch, dtype=torch.int64).pin_memory()
+        self.h_rl = torch.empty(self.batch, dtype=torch.int32).pin_memory()
+        self.d_src = torch.empty(self.batch, dtype=torch.int64, device="cuda")
+        self.d_rl = torch.empty(self.batch, dtype=torch.int32, device="cuda")
+        self.h_out = torch.empty(self.batch * self.data_stride, dtype=torch.uint8).pin_memory()
+        self.pending_error = None
+
+    def feed(self, data):
+        """Append wire bytes (grows the pinned buffer if needed)."""
+        mv = memoryview(data).cast("B")
+        need = self.fill + len(mv)
+        if need > self.h_buf.numel():
+            nb = self.torch.empty(max(need, 2 * self.h_buf.numel()), dtype=self.torch.uint8).pin_memory()
+            nb[:self.fill].copy_(self.h_buf[:self.fill])
+            self.h_buf = nb
+        self.h_buf.numpy()[self.fill:need] = np.frombuffer(mv, np.uint8)
+        self.fill = need
+
+    def _scan(self):
+        lib = _lib.load()
+        consumed = ctypes.c_size_t(0)
+        buf = self.h_buf.numpy()
+        rc = lib.tg_scan_records(buf.ctypes.data, self.fill, self.max_body,
+                                 self.h_off.ctypes.data, self.h_rlen.ctypes.data, self.batch,
+                                 ctypes.byref(consumed))
+        if rc == _lib.TG_EOVERFLOW:
+            n = _count(self.h_rlen, consumed.value)
+            return n, consumed.value, TLSRecordOverflow()
+        if rc == _lib.TG_EHEADER:
+            n = _count(self.h_rlen, consumed.value)
+            return n, consumed.value, TLSIllegalParameterException("Malformed record layer header")
+        _lib.check(rc)
+        return int(rc), consumed.value, None
+
+    def records(self):
+        """Open every complete record fed so far; returns [(type, bytearray)]."""
+        out = []
+        for ct, plen in self._batches():
+            if len(plen) == 0:
+                continue
+            ho = self._rows_to_host(len(plen))
+            for i in range(len(plen)):
+                o = i * self.data_stride
+                out.append((int(ct[i]), bytearray(ho[o:o + int(plen[i])].tobytes())))
+        return out
+
+    def read_application_data(self, out=None):
+        """The bulk path: the plaintext of every application-data record
+        completed so far, concatenated (other content types are dropped, as a
+        caller that reads only application data would).  The records are
+        packed on the device (tg_gather) and copied straight into ``out`` (a
+        writable buffer, filled from offset 0) or a new bytearray; returns
+        that buffer's filled part (bytearray / memoryview).  Raises like
+        records()."""
+        pieces, pos = [], 0
+        dst = None if out is None else np.frombuffer(out, np.uint8)
+        for ct, plen in self._batches():
+            n = len(plen)
+            app = ct == APPLICATION_DATA
+            L = plen.astype(np.int64) * app
+            total = int(L.sum())
+            if total == 0:
+                continue
+            s = self.slot
+            h_dst = self.h_src.numpy()
+            h_dst[0] = 0
+            if n > 1:
+                np.cumsum(L[:-1], out=h_dst[1:n])
+            self.h_rl.numpy()[:n] = L.astype(np.int32)
+            with self.torch.cuda.stream(s.stream):
+                self.d_src[:n].copy_(self.h_src[:n], non_blocking=True)
+                self.d_rl[:n].copy_(self.h_rl[:n], non_blocking=True)
+                gather(s.d_data, s.d_data_off, self.d_rl, s.d_pack, self.d_src, n, stream=s.stream)
+            if dst is not None:
+                if pos + total > len(dst):
+                    raise ValueError("output buffer too small")
+                target = dst[pos:pos + total]
+            else:
+                piece = bytearray(total)
+                pieces.append(piece)
+                target = np.frombuffer(piece, np.uint8)
+            _lib.check(_lib.load().tg_memcpy_d2h(target.ctypes.data, s.d_pack.data_ptr(), total,
+                                                 s.stream.cuda_stream))
+            pos += total
+        if dst is not None:
+            return memoryview(out)[:pos]
+        if len(pieces) == 1:
+            return pieces[0]
+        return bytearray(b"".join(pieces))
+
+    def _batches(self):
+        """Open the complete records batch by batch; yields (ctype, plen) per
+        batch, the plaintexts in the slot's device rows.  An error stops at the failing record: the
+        records before it are yielded, the exception is raised on the next
+        call (at once if there were none)."""
+        if self.pending_error is not None:
+            e, self.pending_error = self.pending_error, None
+            raise e
+        got = False
+        while True:
+            n, used, err = self._scan()
+            if n:
+                res = self._open(n, used)
+                got = got or len(res[1]) > 0
+                yield res
+                if self.pending_error is not None:
+                    if not got:
+                        e, self.pending_error = self.pending_error, None
+                        raise e
+                    return
+            if err is not None:
+                self.fill = 0
+                if got:
+                    self.pending_error = err
+                    return
+                raise err
+            if n < self.batch:
+                return
+
+    def _open(self, n, used):
+        """Open n scanned records on the device; the plaintexts stay in the
+        slot's device rows (i * data_stride).  Returns (ctype, plen) of the
+        records before the first failing one (whose error is kept pending)."""
+        torch = self.torch
+        s = self.slot
+        src = self.h_src.numpy()
+        src[:n] = self.h_off[:n].astype(np.int64)
+        self.h_rl.numpy()[:n] = self.h_rlen[:n].astype(np.int32)
+        with torch.cuda.stream(s.stream):
+            s.d_pack[:used].copy_(self.h_buf[:used], non_blocking=True)
+            self.d_src[:n].copy_(self.h_src[:n], non_blocking=True)
+            self.d_rl[:n].copy_(self.h_rl[:n], non_blocking=True)
+            # wire records into 16-byte aligned slots (payload after header aligned)
+            gather(s.d_pack, self.d_src, self.d_rl, s.d_wire, s.d_wire_off, n, stream=s.stream)
+            open_records(self.key, self.version, self.fixed_iv, self.seq, n, s.d_wire,
+                         s.d_wire_off, self.d_rl, s.d_data, s.d_data_off, s.d_len, s.d_ctype,
+                         s.d_status, stream=s.stream)
+            self.h_plen[:n].copy_(s.d_len[:n], non_blocking=True)
+            s.h_ctype[:n].copy_(s.d_ctype[:n], non_blocking=True)
+            s.h_status[:n].copy_(s.d_status[:n], non_blocking=True)
+            s.event.record(s.stream)
+        s.event.synchronize()
+        # the unconsumed tail to the front (the copy above has read h_buf)
+        tail = self.fill - used
+        if tail:
+            buf = self.h_buf.numpy()
+            buf[:tail] = buf[used:self.fill].copy()
+        self.fill = tail
+        st = s.h_status.numpy()[:n]
+        plen = self.h_plen.numpy()[:n]
+        ct = s.h_ctype.numpy()[:n]
+        bad = np.nonzero(st)[0]
+        k = int(bad[0]) if len(bad) else n
+        if len(bad):
+            cls, msg = _STATUS_EXC.get(int(st[k]), (TLSProtocolException, "record error"))
+            self.pending_error = cls(msg)
+            self.fill = 0
+        self.seq += k
+        return ct[:k].copy(), plen[:k].copy()
+
+    def _rows_to_host(self, k):
+        """Device plaintext rows 0..k-1 -> h_out (pinned), same layout."""
+        s = self.slot
+        span = (k - 1) * self.data_stride + self.max_body
+        with self.torch.cuda.stream(s.stream):
+            self.h_out[:span].copy_(s.d_data[:span], non_blocking=True)
+        s.stream.synchronize()
+        return self.h_out.numpy()
+
+
+def read_application_data(reader):
+    """RecordReader.read_application_data (module-level alias)."""
+    return reader.read_application_data()
+
+
+def _count(rlen, consumed):
+    n, tot = 0, 0
+    while tot < consumed:
+        tot += int(rlen[n])
+        n += 1
+    return n
+
+
+def gather(src, src_off, lens, dst, dst_off, n, stream=None):
+    """tg_gather: copy n byte ranges src[src_off[i]:+len[i]] -> dst[dst_off[i]:]."""
+    from .batch import _stream
+    l = _lib.load()
+    _lib.check(l.tg_gather(_ptr(src, "src"), _ptr(src_off, "src_off"), _ptr(lens, "len"),
+                           _ptr(dst, "dst"), _ptr(dst_off, "dst_off"), int(n), _stream(stream)))
+
+
+def scan_records(buf, max_body, max_n=None):
+    """tg_scan_records on a host buffer: ([(offset, record_len)], consumed);
+    raises TLSRecordOverflow / TLSIllegalParameterException like RecordSocket."""
+    a = np.frombuffer(bytes(buf), np.uint8)
+    max_n = max_n if max_n is not None else max(1, len(a) // 5)
+    off = np.empty(max_n, np.uint64)
+    rl = np.empty(max_n, np.uint32)
+    consumed = ctypes.c_size_t(0)
+    rc = _lib.load().tg_scan_records(a.ctypes.data if len(a) else None, len(a), int(max_body),
+                                     off.ctypes.data, rl.ctypes.data, max_n, ctypes.byref(consumed))
+    if rc == _lib.TG_EOVERFLOW:
+        raise TLSRecordOverflow()
+    if rc == _lib.TG_EHEADER:
+        raise TLSIllegalParameterException("Malformed record layer header")
+    _lib.check(rc)
+    return [(int(off[i]), int(rl[i])) for i in range(rc)], consumed.value
