@@ -758,6 +758,138 @@ int launch_bs(const GcmKeyDev* key, const tg_batch& b, hipStream_t s) {
     return hipGetLastError() == hipSuccess ? TG_OK : TG_EHIP;
 }
 
+// ---- wave-per-record kernel (small batches and the per-record calls) ----
+// One record per wavefront (the layout of the north star): the GHASH input
+// sequence AAD || C || length block, front-padded with zero blocks (neutral
+// for GHASH: y stays 0) to 64 B blocks, is split into 64 contiguous
+// segments of B blocks; lane l encrypts (T-table CTR, counters 2 + c) and
+// hashes its segment by Horner with the table-free multiply (GhashClmul's
+// gf128_mul, H in normal order), and a shuffle tree combines the lanes:
+// at level k the left partner (lower lanes = earlier blocks) becomes
+// Y_left * H^(B 2^k) + Y_right.  A 16 KiB record is 17 blocks per lane
+// instead of 1026 on one lane, so a single record takes tens of
+// microseconds instead of a millisecond and a half.
+constexpr int kWaveThreads = 256;    // four records per workgroup, one per wave
+constexpr size_t kWaveLds = 65536;   // Te0/Te2 copies at LDS 0
+
+__device__ __forceinline__ uint4 shfl_xor4(uint4 v, int m) {
+    return make_uint4((uint32_t)__shfl_xor((int)v.x, m, 64), (uint32_t)__shfl_xor((int)v.y, m, 64),
+                      (uint32_t)__shfl_xor((int)v.z, m, 64), (uint32_t)__shfl_xor((int)v.w, m, 64));
+}
+
+// x^e in GF(2^128), normal order (square and multiply).
+__device__ __forceinline__ uint4 gf128_pow(uint4 x, uint32_t e) {
+    uint4 r = make_uint4(1, 0, 0, 0);
+    while (e) {
+        if (e & 1) r = gf128_mul(r, x);
+        e >>= 1;
+        if (e) x = gf128_mul(x, x);
+    }
+    return r;
+}
+
+template <int NR, bool OPEN>
+__global__ __launch_bounds__(kWaveThreads) void gcm_wave_kernel(const GcmKeyDev* __restrict__ key,
+                                                                tg_batch b) {
+    stage_te(reinterpret_cast<uint32_t*>(g_lds));
+    RkRegs<NR> rk;
+#pragma unroll
+    for (int k = 0; k < 4 * (NR + 1); ++k) rk.w[k] = key->rk[k];
+    __syncthreads();
+    const uint64_t i = (uint64_t)blockIdx.x * (kWaveThreads / 64) + (threadIdx.x >> 6);
+    if (i >= b.n) return;   // whole wave (uniform)
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t lane4 = (lane & 31u) << 2;
+    const uint8_t* in = rec_in(b, i);
+    uint8_t* out = rec_out(b, i);
+    const uint32_t len = rec_len(b, i);
+    const uint8_t* ad = rec_aad(b, i);
+    const uint32_t alen = rec_aad_len(b, i);
+    const bool aligned = (((uintptr_t)in | (uintptr_t)out) & 15) == 0;
+    const uint4 nv = load_partial(b.nonce + 12 * i, 12);
+    const CtrCache cc = ctr_cache<NR>(lane4, rk, nv);
+    const uint32_t na = (alen + 15) >> 4, nc = (len + 15) >> 4, nfull = len >> 4, tail = len & 15;
+    const uint32_t M = na + nc + 1;            // GHASH blocks (aesgcm.py:60-79)
+    const uint32_t B = (M + 63) >> 6, pad = 64 * B - M;
+    // H = M_0[0x80]: the table row of the GCM element 1 (bit-reflected 0x80)
+    const uint4 hw = key->ghash[0x80];
+    const uint4 hn = make_uint4(to_norm(hw.x), to_norm(hw.y), to_norm(hw.z), to_norm(hw.w));
+    const uint64_t abits = (uint64_t)alen << 3, cbits = (uint64_t)len << 3;
+    uint4 y = make_uint4(0, 0, 0, 0);
+    for (uint32_t t = lane * B; t < lane * B + B; ++t) {
+        if (t < pad) continue;                  // leading zero blocks
+        const uint32_t k = t - pad;
+        uint4 x;
+        if (k < na) {
+            const uint32_t m = alen - 16 * k < 16 ? alen - 16 * k : 16;
+            x = load_partial(ad + 16 * k, m);
+        } else if (k < na + nc) {               // CTR block c (python_aes.py:101-116)
+            const uint32_t c = k - na;
+            const uint4 ks = aes_ctr<NR>(lane4, rk, cc, 2u + c);
+            if (c < nfull) {
+                const uint4 d = load16(in + 16 * c, aligned);
+                const uint4 ct = xor4(d, ks);
+                store16(out + 16 * c, ct, aligned);
+                x = OPEN ? d : ct;
+            } else {
+                const uint4 d = load_partial(in + 16 * c, tail);
+                const uint4 ct = mask_tail(xor4(d, ks), tail);
+                store_partial(out + 16 * c, ct, tail);
+                x = OPEN ? d : ct;
+            }
+        } else {                                // be64(8 alen) || be64(8 len) (aesgcm.py:64)
+            x = make_uint4(bswap32((uint32_t)(abits >> 32)), bswap32((uint32_t)abits),
+                           bswap32((uint32_t)(cbits >> 32)), bswap32((uint32_t)cbits));
+        }
+        y = gf128_mul(make_uint4(y.x ^ to_norm(x.x), y.y ^ to_norm(x.y), y.z ^ to_norm(x.z),
+                                 y.w ^ to_norm(x.w)), hn);
+    }
+    uint4 P = gf128_pow(hn, B);
+#pragma unroll
+    for (int k = 0; k < 6; ++k) {
+        const uint4 o = shfl_xor4(y, 1 << k);
+        if ((lane & ((2u << k) - 1u)) == 0) y = xor4(gf128_mul(y, P), o);
+        if (k < 5) P = gf128_mul(P, P);
+    }
+    // lane 0: tag = GHASH ^ E_K(J0) (aesgcm.py:112-122)
+    const uint4 mask = aes_ctr<NR>(lane4, rk, cc, 1u);
+    const uint4 tag = xor4(make_uint4(to_norm(y.x), to_norm(y.y), to_norm(y.z), to_norm(y.w)), mask);
+    const bool tag_aligned = aligned && tail == 0;
+    if (!OPEN) {
+        if (lane == 0) store16(out + len, tag, tag_aligned);
+        return;
+    }
+    // open: compare (aesgcm.py:148-149); a rejected record's plaintext is zeroed
+    uint32_t diff = 0;
+    if (lane == 0) {
+        const uint4 exp = load16(in + len, tag_aligned);
+        diff = (exp.x ^ tag.x) | (exp.y ^ tag.y) | (exp.z ^ tag.z) | (exp.w ^ tag.w);
+        if (b.status) b.status[i] = diff == 0;
+    }
+    diff = (uint32_t)__shfl((int)diff, 0, 64);
+    if (diff) {
+        const uint4 z = make_uint4(0, 0, 0, 0);
+        for (uint32_t c = lane; c < nfull; c += 64) store16(out + 16 * c, z, aligned);
+        if (tail && lane == 0) store_partial(out + 16 * nfull, z, tail);
+    }
+}
+
+template <int NR, bool OPEN>
+int launch_wave(const GcmKeyDev* key, const tg_batch& b, hipStream_t s) {
+    static bool attr_set = false;
+    if (!attr_set) {
+        if (hipFuncSetAttribute((const void*)gcm_wave_kernel<NR, OPEN>,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)kWaveLds) != hipSuccess)
+            return TG_EHIP;
+        attr_set = true;
+    }
+    const uint64_t groups = (b.n + kWaveThreads / 64 - 1) / (kWaveThreads / 64);   // a wave per record
+    if (groups > 0x7fffffffull) return TG_EINVAL;
+    hipLaunchKernelGGL((gcm_wave_kernel<NR, OPEN>), dim3((unsigned)groups), dim3(kWaveThreads), kWaveLds,
+                       s, key, b);
+    return hipGetLastError() == hipSuccess ? TG_OK : TG_EHIP;
+}
+
 // Key-table kernel (many sessions per batch, BASELINE config 4): lane i uses
 // key key_idx[i]; its round keys are staged into a private LDS row (272-byte
 // stride: conflict-free ds_read_b128) and GHASH is the table-free multiply.
@@ -803,7 +935,14 @@ int launch_v(const GcmKeyDev* key, const tg_batch& b, hipStream_t s) {
 //   0 / unset  T-table kernel, G = 4, 1024 threads, 8-bit GHASH tables (fastest
 //              measured: profiles/r01/gcm_variant_sweep.txt, bitsliced_gcm.txt);
 //   1..3       T-table tuning variants;
-//   4          the bitsliced kernel (gcm_bs_kernel).
+//   4          the bitsliced kernel (gcm_bs_kernel);
+//   6          the wave-per-record kernel (gcm_wave_kernel), which is also what
+//              batches of at most kWaveMaxRecords records use.
+// Up to this many records a batch runs one record per wavefront: below a
+// few thousand records a lane per record leaves most of the GPU idle while
+// one lane walks a whole record (profiles/r01/v11_latency_wave_per_record.txt).
+constexpr uint64_t kWaveMaxRecords = 2048;
+
 int variant() {
     const char* e = getenv("TLSGPU_GCM_VARIANT");
     return e ? atoi(e) : 0;
@@ -816,7 +955,11 @@ int launch(const GcmKeyDev* key, const tg_batch& b, hipStream_t s) {
         case 2: return launch_v<NR, OPEN, 2, 1024, 2>(key, b, s);
         case 3: return launch_v<NR, OPEN, 2, 512, 1>(key, b, s);
         case 4: return launch_bs<NR, OPEN>(key, b, s);
-        default: return launch_v<NR, OPEN, 4, 1024, 0>(key, b, s);
+        case 5: return launch_v<NR, OPEN, 4, 1024, 0>(key, b, s);
+        case 6: return launch_wave<NR, OPEN>(key, b, s);
+        default:
+            if (b.n <= kWaveMaxRecords) return launch_wave<NR, OPEN>(key, b, s);
+            return launch_v<NR, OPEN, 4, 1024, 0>(key, b, s);
     }
 }
 

@@ -202,11 +202,17 @@ __device__ __forceinline__ uint4 aes_block(uint32_t lane4, const RK& rkp, uint4 
                       col_last(s2, s3, s0, s1, k.z, lane4), col_last(s3, s0, s1, s2, k.w, lane4));
 }
 
-// Fill the 64 KiB Te0/Te2 copy block (``te`` points at its first word).
+// Fill the 64 KiB Te0/Te2 copy block (``te`` points at its first word):
+// row x = 8 x uint4{Te0[x]} then 8 x uint4{rotl16(Te0[x])}; consecutive
+// threads write consecutive 16-byte slots (conflict-free ds_write_b128) and
+// the 16 threads of a row read the same Te0 entry (one broadcast load).
 __device__ __forceinline__ void stage_te(uint32_t* te) {
-    for (int e = threadIdx.x; e < 256 * 64; e += blockDim.x) {
-        const uint32_t v = c_te.te0[e >> 6];
-        te[e] = (e & 32) ? rotl32(v, 16) : v;
+    uint4* t4 = reinterpret_cast<uint4*>(te);
+#pragma unroll 4
+    for (int e = threadIdx.x; e < 256 * 16; e += blockDim.x) {
+        const uint32_t v = c_te.te0[e >> 4];
+        const uint32_t w = (e & 8) ? rotl32(v, 16) : v;
+        t4[e] = make_uint4(w, w, w, w);
     }
 }
 

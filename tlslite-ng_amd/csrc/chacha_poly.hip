@@ -339,6 +339,157 @@ __global__ __launch_bounds__(kChachaThreads, MINW) void chacha_kernel(
     }
 }
 
+// ---- wave-per-record kernel (small batches and the per-record calls) ----
+// One record per wavefront: lane l takes the payload ChaCha blocks
+// [l Q, (l+1) Q) (counters 1 + q) and runs Poly1305's Horner over its
+// ciphertext 16-byte blocks; since acc = sum_k m_k r^(M-k) over the M
+// blocks of mac_data, each lane's partial result is lifted by
+// r^(blocks after its segment) (square and multiply in the same 26-bit limbs)
+// and the 64 partials are summed by a shuffle tree.  Lane 0 adds the AAD
+// blocks (lifted by r^(nc+1)) and the length block (times r).
+struct F5 {
+    uint32_t h0, h1, h2, h3, h4;
+};
+
+// a * b mod 2^130 - 5, limbs of both < 2^26 (a little above for a's h1)
+__device__ __forceinline__ F5 fmul(const F5& a, const F5& b) {
+    const uint32_t M26 = 0x3ffffffu;
+    const uint32_t s1 = b.h1 * 5, s2 = b.h2 * 5, s3 = b.h3 * 5, s4 = b.h4 * 5;
+    uint64_t d0 = mul64(a.h0, b.h0) + mul64(a.h1, s4) + mul64(a.h2, s3) + mul64(a.h3, s2) + mul64(a.h4, s1);
+    uint64_t d1 = mul64(a.h0, b.h1) + mul64(a.h1, b.h0) + mul64(a.h2, s4) + mul64(a.h3, s3) + mul64(a.h4, s2);
+    uint64_t d2 = mul64(a.h0, b.h2) + mul64(a.h1, b.h1) + mul64(a.h2, b.h0) + mul64(a.h3, s4) + mul64(a.h4, s3);
+    uint64_t d3 = mul64(a.h0, b.h3) + mul64(a.h1, b.h2) + mul64(a.h2, b.h1) + mul64(a.h3, b.h0) + mul64(a.h4, s4);
+    uint64_t d4 = mul64(a.h0, b.h4) + mul64(a.h1, b.h3) + mul64(a.h2, b.h2) + mul64(a.h3, b.h1) + mul64(a.h4, b.h0);
+    F5 r;
+    uint32_t c;
+    c = (uint32_t)(d0 >> 26); r.h0 = (uint32_t)d0 & M26;
+    d1 += c; c = (uint32_t)(d1 >> 26); r.h1 = (uint32_t)d1 & M26;
+    d2 += c; c = (uint32_t)(d2 >> 26); r.h2 = (uint32_t)d2 & M26;
+    d3 += c; c = (uint32_t)(d3 >> 26); r.h3 = (uint32_t)d3 & M26;
+    d4 += c; c = (uint32_t)(d4 >> 26); r.h4 = (uint32_t)d4 & M26;
+    r.h0 += c * 5; c = r.h0 >> 26; r.h0 &= M26;
+    r.h1 += c;
+    return r;
+}
+
+__device__ __forceinline__ F5 fnorm_add(const F5& a, const F5& b) {
+    const uint32_t M26 = 0x3ffffffu;
+    F5 r = {a.h0 + b.h0, a.h1 + b.h1, a.h2 + b.h2, a.h3 + b.h3, a.h4 + b.h4};
+    uint32_t c;
+    c = r.h0 >> 26; r.h0 &= M26; r.h1 += c;
+    c = r.h1 >> 26; r.h1 &= M26; r.h2 += c;
+    c = r.h2 >> 26; r.h2 &= M26; r.h3 += c;
+    c = r.h3 >> 26; r.h3 &= M26; r.h4 += c;
+    c = r.h4 >> 26; r.h4 &= M26; r.h0 += c * 5;
+    c = r.h0 >> 26; r.h0 &= M26; r.h1 += c;
+    return r;
+}
+
+__device__ __forceinline__ F5 fpow(F5 x, uint32_t e) {
+    F5 r = {1, 0, 0, 0, 0};
+    while (e) {
+        if (e & 1) r = fmul(r, x);
+        e >>= 1;
+        if (e) x = fmul(x, x);
+    }
+    return r;
+}
+
+__device__ __forceinline__ F5 fshfl_xor(const F5& v, int m) {
+    return F5{(uint32_t)__shfl_xor((int)v.h0, m, 64), (uint32_t)__shfl_xor((int)v.h1, m, 64),
+              (uint32_t)__shfl_xor((int)v.h2, m, 64), (uint32_t)__shfl_xor((int)v.h3, m, 64),
+              (uint32_t)__shfl_xor((int)v.h4, m, 64)};
+}
+
+template <bool OPEN>
+__global__ __launch_bounds__(256) void chacha_wave_kernel(const ChachaKeyDev* __restrict__ keys,
+                                                          tg_batch b) {
+    const uint64_t i = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6);   // a wave per record
+    if (i >= b.n) return;   // whole wave (uniform)
+    const uint32_t lane = threadIdx.x & 63u;
+    uint32_t k[8];
+#pragma unroll
+    for (int w = 0; w < 8; ++w) k[w] = keys->k[w];
+    const uint8_t* in = rec_in(b, i);
+    uint8_t* out = rec_out(b, i);
+    const uint32_t len = rec_len(b, i);
+    const uint8_t* ad = rec_aad(b, i);
+    const uint32_t alen = rec_aad_len(b, i);
+    const bool aligned = (((uintptr_t)in | (uintptr_t)out) & 15) == 0;
+    const uint4 nv = load_partial(b.nonce + 12 * i, 12);
+    Poly p;
+    {
+        uint32_t otk[16];
+        chacha_block(k, 0, nv.x, nv.y, nv.z, otk);   // poly1305_key_gen (every lane)
+        poly_init(p, otk);
+    }
+    const F5 r = {p.r0, p.r1, p.r2, p.r3, p.r4};
+    const uint32_t nc = (len + 15) >> 4, nf = len >> 4, tail = len & 15;
+    const uint32_t nq = (len + 63) >> 6, Q = (nq + 63) >> 6;
+    const uint32_t q0 = lane * Q, q1 = q0 + Q < nq ? q0 + Q : nq;
+    for (uint32_t q = q0; q < q1; ++q) {            // chacha20_poly1305.py:58-63
+        uint32_t ks[16];
+        chacha_block(k, 1 + q, nv.x, nv.y, nv.z, ks);
+#pragma unroll
+        for (int sb = 0; sb < 4; ++sb) {
+            const uint32_t c = 4 * q + sb;
+            const uint4 kv = make_uint4(ks[4 * sb], ks[4 * sb + 1], ks[4 * sb + 2], ks[4 * sb + 3]);
+            if (c < nf) {
+                const uint4 d = load16(in + 16 * c, aligned);
+                const uint4 ct = xor4(d, kv);
+                store16(out + 16 * c, ct, aligned);
+                poly_block(p, OPEN ? d : ct);
+            } else if (c == nf && tail) {
+                const uint4 d = load_partial(in + 16 * c, tail);
+                const uint4 ct = mask_tail(xor4(d, kv), tail);
+                store_partial(out + 16 * c, ct, tail);
+                poly_block(p, OPEN ? d : ct);
+            }
+        }
+    }
+    // lift the segment: acc_seg * r^(blocks after it, incl. the length block)
+    const uint32_t cb = 4 * q1 < nc ? 4 * q1 : nc;
+    F5 z = fmul(F5{p.h0, p.h1, p.h2, p.h3, p.h4}, fpow(r, nc - cb + 1));
+    if (lane == 0) {
+        Poly pa = p;                                 // the AAD (mac_data starts with it)
+        pa.h0 = pa.h1 = pa.h2 = pa.h3 = pa.h4 = 0;
+        for (uint32_t off = 0; off < alen; off += 16) {
+            const uint32_t m = alen - off < 16 ? alen - off : 16;
+            poly_block(pa, load_partial(ad + off, m));
+        }
+        z = fnorm_add(z, fmul(F5{pa.h0, pa.h1, pa.h2, pa.h3, pa.h4}, fpow(r, nc + 1)));
+        Poly pl = pa;                                // le64(alen) || le64(len), times r
+        pl.h0 = pl.h1 = pl.h2 = pl.h3 = pl.h4 = 0;
+        poly_block(pl, make_uint4(alen, 0, len, 0));
+        z = fnorm_add(z, F5{pl.h0, pl.h1, pl.h2, pl.h3, pl.h4});
+    }
+#pragma unroll
+    for (int m = 1; m < 64; m <<= 1) z = fnorm_add(z, fshfl_xor(z, m));
+    p.h0 = z.h0; p.h1 = z.h1; p.h2 = z.h2; p.h3 = z.h3; p.h4 = z.h4;
+    const uint4 tag = poly_finish(p);                // poly1305.py:47-48
+    const bool tag_aligned = aligned && (len & 15) == 0;
+    if (!OPEN) {
+        if (lane == 0) store16(out + len, tag, tag_aligned);
+        return;
+    }
+    uint32_t diff = 0;
+    if (lane == 0) {
+        const uint4 exp = load16(in + len, tag_aligned);
+        diff = (exp.x ^ tag.x) | (exp.y ^ tag.y) | (exp.z ^ tag.z) | (exp.w ^ tag.w);
+        if (b.status) b.status[i] = diff == 0;
+    }
+    diff = (uint32_t)__shfl((int)diff, 0, 64);
+    if (diff) {                                      // chacha20_poly1305.py:90-91
+        const uint4 zz = make_uint4(0, 0, 0, 0);
+        for (uint32_t c = lane; c < nf; c += 64) store16(out + 16 * c, zz, aligned);
+        if (tail && lane == 0) store_partial(out + 16 * nf, zz, tail);
+    }
+}
+
+// Up to this many records a batch runs one record per wavefront (see the
+// GCM launcher; profiles/r01/v11_latency_wave_per_record.txt).
+constexpr uint64_t kWaveMaxRecords = 2048;
+
 template <bool OPEN, bool MULTIKEY, int MINW>
 int launch_w(const ChachaKeyDev* keys, const tg_batch& b, hipStream_t s) {
     const uint64_t blocks = (b.n + kChachaThreads - 1) / kChachaThreads;
@@ -347,20 +498,25 @@ int launch_w(const ChachaKeyDev* keys, const tg_batch& b, hipStream_t s) {
     return hipGetLastError() == hipSuccess ? TG_OK : TG_EHIP;
 }
 
-// Occupancy variants (TLSGPU_CHACHA_VARIANT, measurement only): minimum
-// waves per SIMD requested from the register allocator.
+// Variants (TLSGPU_CHACHA_VARIANT, read per launch; tests and measurement):
+// 0 = auto (wave per record up to kWaveMaxRecords records, else lane per
+// record), 1 / 2 = lane per record asking for 5 / 6 waves per SIMD,
+// 3 = wave per record, 4 = lane per record.
 int chacha_variant() {
-    static int v = -1;
-    if (v < 0) {
-        const char* e = getenv("TLSGPU_CHACHA_VARIANT");
-        v = e ? atoi(e) : 0;
-    }
-    return v;
+    const char* e = getenv("TLSGPU_CHACHA_VARIANT");
+    return e ? atoi(e) : 0;
 }
 
 template <bool OPEN, bool MULTIKEY>
 int launch(const ChachaKeyDev* keys, const tg_batch& b, hipStream_t s) {
-    switch (chacha_variant()) {
+    const int v = chacha_variant();
+    if (!MULTIKEY && (v == 3 || (v == 0 && b.n <= kWaveMaxRecords))) {
+        const uint64_t groups = (b.n + 3) / 4;
+        if (groups > 0x7fffffffull) return TG_EINVAL;
+        hipLaunchKernelGGL((chacha_wave_kernel<OPEN>), dim3((unsigned)groups), dim3(256), 0, s, keys, b);
+        return hipGetLastError() == hipSuccess ? TG_OK : TG_EHIP;
+    }
+    switch (v) {
         case 1: return launch_w<OPEN, MULTIKEY, 5>(keys, b, s);
         case 2: return launch_w<OPEN, MULTIKEY, 6>(keys, b, s);
         default: return launch_w<OPEN, MULTIKEY, 1>(keys, b, s);
