@@ -104,6 +104,8 @@ def main():
                          "AES-128-GCM seal, 16385-byte inner plaintext, seq-sharded); ingest = "
                          "the host ingest pipeline (tlsgpu.ingest, SURVEY 8(f) row 3), host "
                          "memory to host memory")
+    ap.add_argument("--c4-presorted", action="store_true",
+                    help="config 4: pack records longest first on the host")
     ap.add_argument("--ingest-mib", type=int, default=2048,
                     help="application data per direction for --config ingest")
     args = ap.parse_args()
@@ -331,9 +333,10 @@ def run_config4(args):
     """BASELINE configs[3]: AES-256-GCM, 65 536 independent session keys
     (PCG64 0x7716), 2^20 records with Zipf(1.2) lengths 64 B-16 KiB (PCG64
     0x7717), TLS 1.2 AAD seq||0x17||0x0303||len and nonce iv4||seq.  Records
-    are packed in descending length order (the batch planner's choice: lanes of
-    a wavefront then carry similar lengths).  Reports payload GiB/s of seal and
-    of open, and the byte-weighted mean length."""
+    are packed in arrival (seq) order; the engine's planner (planner.hip)
+    launches them longest first.  --c4-presorted packs them in descending
+    length order on the host instead (what the planner does, for comparison).
+    Reports payload GiB/s of seal and of open, and the byte-weighted mean length."""
     import numpy as np
     import torch
     import tlsgpu
@@ -344,7 +347,7 @@ def run_config4(args):
     key_idx = rk.integers(0, nkeys, n).astype(np.uint32)
     rl = np.random.default_rng(0x7717)
     lens = np.clip(64 * rl.zipf(1.2, n), 64, 16384).astype(np.int64)
-    order = np.argsort(-lens, kind="stable")
+    order = np.argsort(-lens, kind="stable") if args.c4_presorted else np.arange(n)
     lens, key_idx = lens[order], key_idx[order]
     seq = order.astype(np.uint64)           # record identity = its original seq number
     in_sz = (lens + 15) // 16 * 16
@@ -397,6 +400,7 @@ def run_config4(args):
             "value": round(2 * payload / ((res["seal"]["ms"] + res["open"]["ms"]) / 1e3) / 2 ** 30, 2),
             "unit": "GiB/s", "n_gpus": 1, "steps": args.steps, "warmup": args.warmup,
             "dtype": "u8", "data": "synthetic", "records": n, "keys": nkeys,
+            "record_order": "host-presorted" if args.c4_presorted else "arrival (engine planner)",
             "mean_len": round(float(lens.mean()), 1),
             "byte_weighted_mean_len": round(float((lens * lens).sum() / lens.sum()), 1),
             "per_op": res, "verified": bool(ok)}

@@ -73,3 +73,24 @@ def test_auto_wave_per_record_batch(torch, tg, oracle_mod, alg, klen):
     obj = tg.HipAESGCM(bytearray(key)) if alg == "aesgcm" else tg.HipCHACHA20_POLY1305(bytearray(key))
     run_seal_open(torch, tg, oracle_mod, hb, alg, np.frombuffer(key, np.uint8), obj,
                   tamper=(0, 2047))
+
+
+@pytest.mark.parametrize("alg,klen,keys", [("aesgcm", 16, 1), ("chacha", 32, 1),
+                                          ("aesgcm", 32, 29), ("chacha", 32, 29)])
+@pytest.mark.parametrize("align", [16, 1])
+def test_planned_mixed_batch(torch, tg, oracle_mod, alg, klen, keys, align):
+    """> 2048 records with per-record lengths run longest first (planner.hip):
+    every record must still land in its own output slot."""
+    from batchpack import HostBatch, run_seal_open
+    rng = np.random.default_rng(1000 + klen + keys + align)
+    lens = list(rng.integers(0, 3000, 5000)) + [16384, 16400, 0, 1] * 5
+    hb = HostBatch(lens, payload_seed=align, align=align, aad_mode="tls12", key_count=keys)
+    kb = [rng.bytes(klen) for _ in range(keys)]
+    if keys == 1:
+        obj = tg.HipAESGCM(bytearray(kb[0])) if alg == "aesgcm" else \
+            tg.HipCHACHA20_POLY1305(bytearray(kb[0]))
+        karr = np.frombuffer(kb[0], np.uint8)
+    else:
+        obj = tg.KeyTable("chacha20-poly1305" if alg == "chacha" else "aesgcm", kb)
+        karr = np.frombuffer(b"".join(kb), np.uint8).reshape(keys, klen)
+    run_seal_open(torch, tg, oracle_mod, hb, alg, karr, obj, tamper=(7, 2500, 5019))

@@ -370,7 +370,7 @@ __device__ __forceinline__ void gcm_record(const tg_batch& b, uint64_t i, uint32
 // 1 = GhashTablesRot, 2 = GhashTablesRotLds; GH / 10 = 1 adds the SPLIT fence.
 template <int NR, bool OPEN, int G, int THREADS, int GH>
 __global__ __launch_bounds__(THREADS) void gcm_kernel(const GcmKeyDev* __restrict__ key,
-                                                      tg_batch b) {
+                                                      tg_batch b, const uint32_t* __restrict__ order) {
     constexpr int GHK = GH % 10, SPLIT = GH / 10;   // GHASH flavour, split schedule
     constexpr bool ROT = GHK != 0;
     uint4* lds = g_lds;
@@ -393,8 +393,9 @@ __global__ __launch_bounds__(THREADS) void gcm_kernel(const GcmKeyDev* __restric
     for (int k = 0; k < 4 * (NR + 1); ++k) rk.w[k] = key->rk[k];
     __syncthreads();
 
-    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= b.n) return;
+    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= b.n) return;
+    const uint64_t i = order ? order[t] : t;
     const uint32_t lane4 = ((threadIdx.x & 31u) << 2) | kTeBase;
     if constexpr (GHK == 0) {
         gcm_record<NR, OPEN, G, RkRegs<NR>, GhashTables, SPLIT>(b, i, lane4, rk, GhashTables{});
@@ -899,12 +900,14 @@ constexpr size_t kMkLds = 65536 + kMkThreads * kMkRowBytes;
 
 template <int NR, bool OPEN, int G>
 __global__ __launch_bounds__(kMkThreads, 4) void gcm_table_kernel(const GcmTableKey* __restrict__ keys,
-                                                              tg_batch b) {
+                                                              tg_batch b,
+                                                              const uint32_t* __restrict__ order) {
     uint4* lds = g_lds;
     stage_te(reinterpret_cast<uint32_t*>(lds));  // Te0/Te2 copies at LDS 0
     __syncthreads();
-    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= b.n) return;
+    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= b.n) return;
+    const uint64_t i = order ? order[t] : t;
     const GcmTableKey* kp = keys + b.key_idx[i];
     const RkLds rk{65536u + threadIdx.x * kMkRowBytes};
     uint4* row = lds + rk.base / 16;
@@ -916,7 +919,7 @@ __global__ __launch_bounds__(kMkThreads, 4) void gcm_table_kernel(const GcmTable
 }
 
 template <int NR, bool OPEN, int G, int THREADS, int GH>
-int launch_v(const GcmKeyDev* key, const tg_batch& b, hipStream_t s) {
+int launch_v(const GcmKeyDev* key, const tg_batch& b, hipStream_t s, const uint32_t* order) {
     static bool attr_set = false;
     if (!attr_set) {
         if (hipFuncSetAttribute((const void*)gcm_kernel<NR, OPEN, G, THREADS, GH>,
@@ -927,7 +930,7 @@ int launch_v(const GcmKeyDev* key, const tg_batch& b, hipStream_t s) {
     }
     const uint64_t blocks = (b.n + THREADS - 1) / THREADS;
     hipLaunchKernelGGL((gcm_kernel<NR, OPEN, G, THREADS, GH>), dim3((unsigned)blocks), dim3(THREADS),
-                       kGcmLds, s, key, b);
+                       kGcmLds, s, key, b, order);
     return hipGetLastError() == hipSuccess ? TG_OK : TG_EHIP;
 }
 
@@ -949,22 +952,22 @@ int variant() {
 }
 
 template <int NR, bool OPEN>
-int launch(const GcmKeyDev* key, const tg_batch& b, hipStream_t s) {
+int launch(const GcmKeyDev* key, const tg_batch& b, hipStream_t s, const uint32_t* order) {
     switch (variant()) {   // profiles/r01/gcm_variant_sweep.txt
-        case 1: return launch_v<NR, OPEN, 2, 1024, 0>(key, b, s);
-        case 2: return launch_v<NR, OPEN, 2, 1024, 2>(key, b, s);
-        case 3: return launch_v<NR, OPEN, 2, 512, 1>(key, b, s);
+        case 1: return launch_v<NR, OPEN, 2, 1024, 0>(key, b, s, order);
+        case 2: return launch_v<NR, OPEN, 2, 1024, 2>(key, b, s, order);
+        case 3: return launch_v<NR, OPEN, 2, 512, 1>(key, b, s, order);
         case 4: return launch_bs<NR, OPEN>(key, b, s);
-        case 5: return launch_v<NR, OPEN, 4, 1024, 0>(key, b, s);
+        case 5: return launch_v<NR, OPEN, 4, 1024, 0>(key, b, s, order);
         case 6: return launch_wave<NR, OPEN>(key, b, s);
         default:
             if (b.n <= kWaveMaxRecords) return launch_wave<NR, OPEN>(key, b, s);
-            return launch_v<NR, OPEN, 4, 1024, 0>(key, b, s);
+            return launch_v<NR, OPEN, 4, 1024, 0>(key, b, s, order);
     }
 }
 
 template <int NR, bool OPEN>
-int launch_table(const GcmTableKey* keys, const tg_batch& b, hipStream_t s) {
+int launch_table(const GcmTableKey* keys, const tg_batch& b, hipStream_t s, const uint32_t* order) {
     static bool attr_set = false;
     if (!attr_set) {
         if (hipFuncSetAttribute((const void*)gcm_table_kernel<NR, OPEN, 1>,
@@ -975,7 +978,7 @@ int launch_table(const GcmTableKey* keys, const tg_batch& b, hipStream_t s) {
     }
     const uint64_t blocks = (b.n + kMkThreads - 1) / kMkThreads;
     hipLaunchKernelGGL((gcm_table_kernel<NR, OPEN, 1>), dim3((unsigned)blocks), dim3(kMkThreads),
-                       kMkLds, s, keys, b);  // G = 1: one block in flight per lane
+                       kMkLds, s, keys, b, order);  // G = 1: one block in flight per lane
     return hipGetLastError() == hipSuccess ? TG_OK : TG_EHIP;
 }
 
@@ -983,17 +986,21 @@ int launch_table(const GcmTableKey* keys, const tg_batch& b, hipStream_t s) {
 }  // namespace tg
 
 int tg_launch_gcm_table(const tg::GcmTableKey* keys, int rounds, const tg_batch& b, bool open,
-                        hipStream_t s) {
+                        hipStream_t s, const uint32_t* order) {
     if (rounds == 10)
-        return open ? tg::launch_table<10, true>(keys, b, s) : tg::launch_table<10, false>(keys, b, s);
+        return open ? tg::launch_table<10, true>(keys, b, s, order)
+                    : tg::launch_table<10, false>(keys, b, s, order);
     if (rounds == 14)
-        return open ? tg::launch_table<14, true>(keys, b, s) : tg::launch_table<14, false>(keys, b, s);
+        return open ? tg::launch_table<14, true>(keys, b, s, order)
+                    : tg::launch_table<14, false>(keys, b, s, order);
     return TG_EINVAL;
 }
 
 int tg_launch_gcm(const tg::GcmKeyDev* key, int rounds, const tg_batch& b, bool open,
-                  hipStream_t s) {
-    if (rounds == 10) return open ? tg::launch<10, true>(key, b, s) : tg::launch<10, false>(key, b, s);
-    if (rounds == 14) return open ? tg::launch<14, true>(key, b, s) : tg::launch<14, false>(key, b, s);
+                  hipStream_t s, const uint32_t* order) {
+    if (rounds == 10)
+        return open ? tg::launch<10, true>(key, b, s, order) : tg::launch<10, false>(key, b, s, order);
+    if (rounds == 14)
+        return open ? tg::launch<14, true>(key, b, s, order) : tg::launch<14, false>(key, b, s, order);
     return TG_EINVAL;
 }

@@ -202,16 +202,44 @@ size_t dev_key_bytes(const tg_key* k) {
     return k->nkeys > 1 ? sizeof(tg::GcmTableKey) * k->nkeys : sizeof(tg::GcmKeyDev);
 }
 
+// Batches large enough for the lane-per-record kernels with per-record
+// lengths run longest first (planner.hip): a wave then holds records of
+// nearly one length instead of idling behind its longest.
+constexpr uint64_t kPlanMinRecords = 2049;
+
+// The order and the sort's scratch are allocated stream-ordered on the
+// launch's stream (hipMallocAsync / hipFreeAsync), so batches in flight on
+// other streams never share them.
+int launch_kernels(tg_key* k, const tg_batch& b, bool open, hipStream_t s, const uint32_t* order);
+
 int launch(tg_key* k, const tg_batch& b, bool open, hipStream_t s) {
+    const char* e = getenv("TLSGPU_NO_PLAN");
+    if (!b.len || b.n < kPlanMinRecords || is_ccm(k->alg) || b.n > 0xffffffffull || (e && atoi(e)))
+        return launch_kernels(k, b, open, s, nullptr);
+    size_t scratch = 0;
+    int rc = tg_length_order(b.len, b.n, nullptr, nullptr, &scratch, s);
+    if (rc) return rc;
+    const size_t obytes = (b.n * sizeof(uint32_t) + 255) & ~(size_t)255;
+    uint8_t* buf = nullptr;
+    HIP_TRY(hipMallocAsync((void**)&buf, obytes + scratch, s));
+    uint32_t* order = reinterpret_cast<uint32_t*>(buf);
+    rc = tg_length_order(b.len, b.n, order, buf + obytes, &scratch, s);
+    if (!rc) rc = launch_kernels(k, b, open, s, order);
+    (void)hipFreeAsync(buf, s);
+    return rc;
+}
+
+int launch_kernels(tg_key* k, const tg_batch& b, bool open, hipStream_t s, const uint32_t* order) {
     if (is_ccm(k->alg))
         return tg_launch_ccm(static_cast<const tg::AesKeyDev*>(k->dev_key), k->nkeys > 1,
                              k->rounds, k->taglen, b, open, s);
     if (k->alg == TG_AES_GCM && k->nkeys > 1)
         return tg_launch_gcm_table(static_cast<const tg::GcmTableKey*>(k->dev_key), k->rounds, b,
-                                   open, s);
+                                   open, s, order);
     if (k->alg == TG_AES_GCM)
-        return tg_launch_gcm(static_cast<const tg::GcmKeyDev*>(k->dev_key), k->rounds, b, open, s);
-    return tg_launch_chacha(static_cast<const tg::ChachaKeyDev*>(k->dev_key), b, open, s);
+        return tg_launch_gcm(static_cast<const tg::GcmKeyDev*>(k->dev_key), k->rounds, b, open, s,
+                             order);
+    return tg_launch_chacha(static_cast<const tg::ChachaKeyDev*>(k->dev_key), b, open, s, order);
 }
 
 size_t align16(size_t v) { return (v + 15) & ~(size_t)15; }

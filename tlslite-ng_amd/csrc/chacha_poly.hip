@@ -249,7 +249,7 @@ __device__ __forceinline__ void tiled_blocks(WaveTile& t, uint32_t lane, uint32_
 
 template <bool OPEN, bool MULTIKEY, int MINW>
 __global__ __launch_bounds__(kChachaThreads, MINW) void chacha_kernel(
-    const ChachaKeyDev* __restrict__ keys, tg_batch b) {
+    const ChachaKeyDev* __restrict__ keys, tg_batch b, const uint32_t* __restrict__ order) {
     __shared__ WaveTile tiles[kWavesPerGroup];
     const uint64_t i_raw = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const uint32_t lane = threadIdx.x & 63;
@@ -258,7 +258,8 @@ __global__ __launch_bounds__(kChachaThreads, MINW) void chacha_kernel(
     // Lanes past the end of the batch stay alive to serve the wave's
     // coalesced transfers, but work on a clamped record and never store.
     const bool valid = i_raw < b.n;
-    const uint64_t i = valid ? i_raw : b.n - 1;
+    const uint64_t t = valid ? i_raw : b.n - 1;
+    const uint64_t i = order ? order[t] : t;   // planner.hip: records longest first
     const uint32_t nvalid = b.n - wave_base < 64 ? (uint32_t)(b.n - wave_base) : 64u;
     uint32_t k[8];
     const ChachaKeyDev* kp = keys + (MULTIKEY ? b.key_idx[i] : 0);
@@ -491,10 +492,10 @@ __global__ __launch_bounds__(256) void chacha_wave_kernel(const ChachaKeyDev* __
 constexpr uint64_t kWaveMaxRecords = 2048;
 
 template <bool OPEN, bool MULTIKEY, int MINW>
-int launch_w(const ChachaKeyDev* keys, const tg_batch& b, hipStream_t s) {
+int launch_w(const ChachaKeyDev* keys, const tg_batch& b, hipStream_t s, const uint32_t* order) {
     const uint64_t blocks = (b.n + kChachaThreads - 1) / kChachaThreads;
     hipLaunchKernelGGL((chacha_kernel<OPEN, MULTIKEY, MINW>), dim3((unsigned)blocks),
-                       dim3(kChachaThreads), 0, s, keys, b);
+                       dim3(kChachaThreads), 0, s, keys, b, order);
     return hipGetLastError() == hipSuccess ? TG_OK : TG_EHIP;
 }
 
@@ -508,7 +509,7 @@ int chacha_variant() {
 }
 
 template <bool OPEN, bool MULTIKEY>
-int launch(const ChachaKeyDev* keys, const tg_batch& b, hipStream_t s) {
+int launch(const ChachaKeyDev* keys, const tg_batch& b, hipStream_t s, const uint32_t* order) {
     const int v = chacha_variant();
     if (!MULTIKEY && (v == 3 || (v == 0 && b.n <= kWaveMaxRecords))) {
         const uint64_t groups = (b.n + 3) / 4;
@@ -517,9 +518,9 @@ int launch(const ChachaKeyDev* keys, const tg_batch& b, hipStream_t s) {
         return hipGetLastError() == hipSuccess ? TG_OK : TG_EHIP;
     }
     switch (v) {
-        case 1: return launch_w<OPEN, MULTIKEY, 5>(keys, b, s);
-        case 2: return launch_w<OPEN, MULTIKEY, 6>(keys, b, s);
-        default: return launch_w<OPEN, MULTIKEY, 1>(keys, b, s);
+        case 1: return launch_w<OPEN, MULTIKEY, 5>(keys, b, s, order);
+        case 2: return launch_w<OPEN, MULTIKEY, 6>(keys, b, s, order);
+        default: return launch_w<OPEN, MULTIKEY, 1>(keys, b, s, order);
     }
 }
 
@@ -546,10 +547,12 @@ __global__ void nonce_kernel(int mode, uint4 iv, uint64_t seq0, uint64_t n, uint
 }  // namespace
 }  // namespace tg
 
-int tg_launch_chacha(const tg::ChachaKeyDev* keys, const tg_batch& b, bool open, hipStream_t s) {
+int tg_launch_chacha(const tg::ChachaKeyDev* keys, const tg_batch& b, bool open, hipStream_t s,
+                     const uint32_t* order) {
     const bool multi = b.key_idx != nullptr;
-    if (open) return multi ? tg::launch<true, true>(keys, b, s) : tg::launch<true, false>(keys, b, s);
-    return multi ? tg::launch<false, true>(keys, b, s) : tg::launch<false, false>(keys, b, s);
+    if (open)
+        return multi ? tg::launch<true, true>(keys, b, s, order) : tg::launch<true, false>(keys, b, s, order);
+    return multi ? tg::launch<false, true>(keys, b, s, order) : tg::launch<false, false>(keys, b, s, order);
 }
 
 int tg_launch_nonces(int mode, const uint8_t* iv_host, uint64_t seq0, uint64_t n, uint8_t* out,

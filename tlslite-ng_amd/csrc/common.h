@@ -147,13 +147,18 @@ struct RecScratch {
 }  // namespace tg
 
 // Launchers implemented in the kernel files (host side).
+// order: NULL, or the processing order of the records (planner.hip): thread
+// t of a lane-per-record kernel handles record order[t].
 int tg_launch_gcm(const tg::GcmKeyDev* key, int rounds, const tg_batch& b, bool open,
-                  hipStream_t s);
+                  hipStream_t s, const uint32_t* order = nullptr);
 int tg_launch_gcm_table(const tg::GcmTableKey* keys, int rounds, const tg_batch& b, bool open,
-                        hipStream_t s);
+                        hipStream_t s, const uint32_t* order = nullptr);
+int tg_length_order(const uint32_t* len, uint64_t n, uint32_t* order, void* scratch, size_t* bytes,
+                    hipStream_t s);
 int tg_launch_ccm(const tg::AesKeyDev* keys, bool table, int rounds, int taglen,
                   const tg_batch& b, bool open, hipStream_t s);
-int tg_launch_chacha(const tg::ChachaKeyDev* keys, const tg_batch& b, bool open, hipStream_t s);
+int tg_launch_chacha(const tg::ChachaKeyDev* keys, const tg_batch& b, bool open, hipStream_t s,
+                     const uint32_t* order = nullptr);
 int tg_launch_records_prep(const tg_records& r, bool seal, bool aes, int taglen,
                            const tg::RecScratch& s, hipStream_t st);
 int tg_launch_records_finish(const tg_records& r, const tg::RecScratch& s, hipStream_t st);
