@@ -892,8 +892,10 @@ int launch_wave(const GcmKeyDev* key, const tg_batch& b, hipStream_t s) {
 }
 
 // Key-table kernel (many sessions per batch, BASELINE config 4): lane i uses
-// key key_idx[i]; its round keys are staged into a private LDS row (272-byte
-// stride: conflict-free ds_read_b128) and GHASH is the table-free multiply.
+// key key_idx[i] and GHASH is the table-free multiply.  This first layout
+// stages each lane's round keys into a private LDS row (272-byte stride:
+// conflict-free ds_read_b128); gcm_table_vkernel below keeps them in VGPRs
+// and is the default.
 constexpr int kMkThreads = 256;
 constexpr uint32_t kMkRowBytes = 272;
 constexpr size_t kMkLds = 65536 + kMkThreads * kMkRowBytes;
@@ -916,6 +918,48 @@ __global__ __launch_bounds__(kMkThreads, 4) void gcm_table_kernel(const GcmTable
     const GhashClmul gh{*reinterpret_cast<const uint4*>(kp->hn)};
     const uint32_t lane4 = (threadIdx.x & 31u) << 2;
     gcm_record<NR, OPEN, G>(b, i, lane4, rk, gh);
+}
+
+// Key-table kernel with the lane's round keys in VGPRs (60 words for
+// AES-256) instead of an LDS row: LDS holds only the 64 KiB Te block, so a
+// 768-thread workgroup (three waves per SIMD) fits where the LDS-row layout
+// (64 KiB + 68 KiB of rows) allowed one wave per SIMD.
+template <int NR, bool OPEN, int THREADS>
+__global__ __launch_bounds__(THREADS) void gcm_table_vkernel(const GcmTableKey* __restrict__ keys,
+                                                             tg_batch b,
+                                                             const uint32_t* __restrict__ order) {
+    stage_te(reinterpret_cast<uint32_t*>(g_lds));   // Te0/Te2 copies at LDS 0
+    __syncthreads();
+    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= b.n) return;
+    const uint64_t i = order ? order[t] : t;
+    const GcmTableKey* kp = keys + b.key_idx[i];
+    RkRegs<NR> rk;   // per-lane values: VGPRs
+#pragma unroll
+    for (int k = 0; k < 4 * (NR + 1); ++k) rk.w[k] = kp->rk[k];
+    const GhashClmul gh{*reinterpret_cast<const uint4*>(kp->hn)};
+    const uint32_t lane4 = (threadIdx.x & 31u) << 2;
+    gcm_record<NR, OPEN, 1>(b, i, lane4, rk, gh);
+}
+
+template <int NR, bool OPEN, int THREADS>
+int launch_table_v(const GcmTableKey* keys, const tg_batch& b, hipStream_t s, const uint32_t* order) {
+    static bool attr_set = false;
+    if (!attr_set) {
+        if (hipFuncSetAttribute((const void*)gcm_table_vkernel<NR, OPEN, THREADS>,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, 65536) != hipSuccess)
+            return TG_EHIP;
+        attr_set = true;
+    }
+    const uint64_t blocks = (b.n + THREADS - 1) / THREADS;
+    hipLaunchKernelGGL((gcm_table_vkernel<NR, OPEN, THREADS>), dim3((unsigned)blocks), dim3(THREADS),
+                       65536, s, keys, b, order);
+    return hipGetLastError() == hipSuccess ? TG_OK : TG_EHIP;
+}
+
+int table_variant() {
+    const char* e = getenv("TLSGPU_GCM_TABLE_VARIANT");
+    return e ? atoi(e) : 0;
 }
 
 template <int NR, bool OPEN, int G, int THREADS, int GH>
@@ -968,6 +1012,15 @@ int launch(const GcmKeyDev* key, const tg_batch& b, hipStream_t s, const uint32_
 
 template <int NR, bool OPEN>
 int launch_table(const GcmTableKey* keys, const tg_batch& b, hipStream_t s, const uint32_t* order) {
+    // TLSGPU_GCM_TABLE_VARIANT (measurement): 0 = round keys in VGPRs, 768
+    // threads (config 4: 368 GiB/s); 2 = the same at 512 threads (346);
+    // 3 = at 1024 threads (217, spills); 9 = round keys in LDS rows (230).
+    switch (table_variant()) {
+        case 2: return launch_table_v<NR, OPEN, 512>(keys, b, s, order);
+        case 3: return launch_table_v<NR, OPEN, 1024>(keys, b, s, order);
+        case 9: break;
+        default: return launch_table_v<NR, OPEN, 768>(keys, b, s, order);
+    }
     static bool attr_set = false;
     if (!attr_set) {
         if (hipFuncSetAttribute((const void*)gcm_table_kernel<NR, OPEN, 1>,
