@@ -188,7 +188,7 @@ int ensure_stage(tg_key* k, size_t bytes) {
     k->h_stage = nullptr;
     k->d_stage = nullptr;
     k->stage_cap = 0;
-    HIP_TRY(hipHostMalloc((void**)&k->h_stage, cap, hipHostMallocDefault));
+    HIP_TRY(hipHostMalloc((void**)&k->h_stage, cap, hipHostMallocMapped));
     HIP_TRY(hipMalloc((void**)&k->d_stage, cap));
     k->stage_cap = cap;
     return TG_OK;
@@ -267,20 +267,34 @@ int single(tg_key* k, const uint8_t* nonce, size_t noncelen, const uint8_t* aad,
     memcpy(k->h_stage, nonce, 12);
     if (aadlen) memcpy(k->h_stage + o_aad, aad, aadlen);
     if (inlen) memcpy(k->h_stage + o_in, in, inlen);
-    HIP_TRY(hipMemcpyAsync(k->d_stage, k->h_stage, o_out, hipMemcpyHostToDevice, k->stream));
+    // Zero copy by default: the kernel reads and writes the mapped pinned
+    // staging buffer over PCIe, so a record costs one launch and one
+    // synchronisation instead of two copies more (TLSGPU_STAGE_COPY=1: copy
+    // through device memory instead).
+    const char* ce = getenv("TLSGPU_STAGE_COPY");
+    const bool copy = ce && atoi(ce);
+    uint8_t* base = k->d_stage;
+    if (!copy) {
+        void* dp = nullptr;
+        HIP_TRY(hipHostGetDevicePointer(&dp, k->h_stage, 0));
+        base = static_cast<uint8_t*>(dp);
+    } else {
+        HIP_TRY(hipMemcpyAsync(k->d_stage, k->h_stage, o_out, hipMemcpyHostToDevice, k->stream));
+    }
     tg_batch b;
     memset(&b, 0, sizeof(b));
     b.n = 1;
-    b.in = k->d_stage + o_in;
+    b.in = base + o_in;
     b.fixed_len = (uint32_t)len;
     b.fixed_aad_len = (uint32_t)aadlen;
-    b.out = k->d_stage + o_out;
-    b.nonce = k->d_stage;
-    b.aad = k->d_stage + o_aad;
-    b.status = open ? k->d_stage + o_st : nullptr;
+    b.out = base + o_out;
+    b.nonce = base;
+    b.aad = base + o_aad;
+    b.status = open ? base + o_st : nullptr;
     if ((rc = launch(k, b, open, k->stream))) return fail(rc, "kernel launch failed");
-    HIP_TRY(hipMemcpyAsync(k->h_stage + o_out, k->d_stage + o_out, total - o_out,
-                           hipMemcpyDeviceToHost, k->stream));
+    if (copy)
+        HIP_TRY(hipMemcpyAsync(k->h_stage + o_out, k->d_stage + o_out, total - o_out,
+                               hipMemcpyDeviceToHost, k->stream));
     HIP_TRY(hipStreamSynchronize(k->stream));
     if (open) {
         const int ok = k->h_stage[o_st] == 1;
