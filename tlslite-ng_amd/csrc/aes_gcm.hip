@@ -764,21 +764,26 @@ int launch_bs(const GcmKeyDev* key, const tg_batch& b, hipStream_t s) {
 // sequence AAD || C || length block, front-padded with zero blocks (neutral
 // for GHASH: y stays 0) to 64 B blocks, is split into 64 contiguous
 // segments of B blocks; lane l encrypts (T-table CTR, counters 2 + c) and
-// hashes its segment by Horner with the table-free multiply (GhashClmul's
-// gf128_mul, H in normal order), and a shuffle tree combines the lanes:
-// at level k the left partner (lower lanes = earlier blocks) becomes
-// Y_left * H^(B 2^k) + Y_right.  A 16 KiB record is 17 blocks per lane
-// instead of 1026 on one lane, so a single record takes tens of
-// microseconds instead of a millisecond and a half.
-constexpr int kWaveThreads = 256;    // four records per workgroup, one per wave
-constexpr size_t kWaveLds = 65536;   // Te0/Te2 copies at LDS 0
+// hashes its segment by Horner with the 8-bit GHASH tables in LDS.  Since
+// GHASH = sum_t X_t H^(64B - t), the lane's value is lifted by
+// H^(B (63 - l)) -- one table-free multiply by a power read from the key's
+// H^e table (GcmKeyDev::hpow) -- and the 64 lifted values are XOR-reduced
+// by shuffles.  A 16 KiB record is 17 blocks per lane instead of 1026 on
+// one lane.  Four records per 256-thread workgroup.
+constexpr int kWaveThreads = 256;
+constexpr size_t kWaveLds = 2 * 65536;   // GHASH tables at 0, Te0/Te2 copies at 64 KiB
 
 __device__ __forceinline__ uint4 shfl_xor4(uint4 v, int m) {
     return make_uint4((uint32_t)__shfl_xor((int)v.x, m, 64), (uint32_t)__shfl_xor((int)v.y, m, 64),
                       (uint32_t)__shfl_xor((int)v.z, m, 64), (uint32_t)__shfl_xor((int)v.w, m, 64));
 }
 
-// x^e in GF(2^128), normal order (square and multiply).
+__device__ __forceinline__ uint4 norm4(uint4 v) {
+    return make_uint4(to_norm(v.x), to_norm(v.y), to_norm(v.z), to_norm(v.w));
+}
+
+// x^e in GF(2^128), normal order (square and multiply): powers beyond the
+// key's table (records over ~18 KiB of AAD + payload).
 __device__ __forceinline__ uint4 gf128_pow(uint4 x, uint32_t e) {
     uint4 r = make_uint4(1, 0, 0, 0);
     while (e) {
@@ -792,7 +797,9 @@ __device__ __forceinline__ uint4 gf128_pow(uint4 x, uint32_t e) {
 template <int NR, bool OPEN>
 __global__ __launch_bounds__(kWaveThreads) void gcm_wave_kernel(const GcmKeyDev* __restrict__ key,
                                                                 tg_batch b) {
-    stage_te(reinterpret_cast<uint32_t*>(g_lds));
+    uint4* lds = g_lds;
+    for (int e = threadIdx.x; e < kGhashEntries; e += blockDim.x) lds[e] = key->ghash[e];
+    stage_te(reinterpret_cast<uint32_t*>(lds) + kTeBase / 4);
     RkRegs<NR> rk;
 #pragma unroll
     for (int k = 0; k < 4 * (NR + 1); ++k) rk.w[k] = key->rk[k];
@@ -800,7 +807,7 @@ __global__ __launch_bounds__(kWaveThreads) void gcm_wave_kernel(const GcmKeyDev*
     const uint64_t i = (uint64_t)blockIdx.x * (kWaveThreads / 64) + (threadIdx.x >> 6);
     if (i >= b.n) return;   // whole wave (uniform)
     const uint32_t lane = threadIdx.x & 63u;
-    const uint32_t lane4 = (lane & 31u) << 2;
+    const uint32_t lane4 = ((lane & 31u) << 2) | kTeBase;
     const uint8_t* in = rec_in(b, i);
     uint8_t* out = rec_out(b, i);
     const uint32_t len = rec_len(b, i);
@@ -812,9 +819,6 @@ __global__ __launch_bounds__(kWaveThreads) void gcm_wave_kernel(const GcmKeyDev*
     const uint32_t na = (alen + 15) >> 4, nc = (len + 15) >> 4, nfull = len >> 4, tail = len & 15;
     const uint32_t M = na + nc + 1;            // GHASH blocks (aesgcm.py:60-79)
     const uint32_t B = (M + 63) >> 6, pad = 64 * B - M;
-    // H = M_0[0x80]: the table row of the GCM element 1 (bit-reflected 0x80)
-    const uint4 hw = key->ghash[0x80];
-    const uint4 hn = make_uint4(to_norm(hw.x), to_norm(hw.y), to_norm(hw.z), to_norm(hw.w));
     const uint64_t abits = (uint64_t)alen << 3, cbits = (uint64_t)len << 3;
     uint4 y = make_uint4(0, 0, 0, 0);
     for (uint32_t t = lane * B; t < lane * B + B; ++t) {
@@ -842,19 +846,21 @@ __global__ __launch_bounds__(kWaveThreads) void gcm_wave_kernel(const GcmKeyDev*
             x = make_uint4(bswap32((uint32_t)(abits >> 32)), bswap32((uint32_t)abits),
                            bswap32((uint32_t)(cbits >> 32)), bswap32((uint32_t)cbits));
         }
-        y = gf128_mul(make_uint4(y.x ^ to_norm(x.x), y.y ^ to_norm(x.y), y.z ^ to_norm(x.z),
-                                 y.w ^ to_norm(x.w)), hn);
+        y = gmul(xor4(y, x));
     }
-    uint4 P = gf128_pow(hn, B);
+    // lift by H^(B (63 - lane)) and XOR-reduce the 64 lanes
+    uint4 yn = norm4(y);
+    const uint32_t e = B * (63u - lane);
+    if (e && (y.x | y.y | y.z | y.w)) {
+        const uint4 hp = e <= (uint32_t)kHPow ? key->hpow[e - 1]
+                                              : gf128_pow(key->hpow[0], e);
+        yn = gf128_mul(yn, hp);
+    }
 #pragma unroll
-    for (int k = 0; k < 6; ++k) {
-        const uint4 o = shfl_xor4(y, 1 << k);
-        if ((lane & ((2u << k) - 1u)) == 0) y = xor4(gf128_mul(y, P), o);
-        if (k < 5) P = gf128_mul(P, P);
-    }
-    // lane 0: tag = GHASH ^ E_K(J0) (aesgcm.py:112-122)
+    for (int m = 1; m < 64; m <<= 1) yn = xor4(yn, shfl_xor4(yn, m));
+    // tag = GHASH ^ E_K(J0) (aesgcm.py:112-122)
     const uint4 mask = aes_ctr<NR>(lane4, rk, cc, 1u);
-    const uint4 tag = xor4(make_uint4(to_norm(y.x), to_norm(y.y), to_norm(y.z), to_norm(y.w)), mask);
+    const uint4 tag = xor4(norm4(yn), mask);
     const bool tag_aligned = aligned && tail == 0;
     if (!OPEN) {
         if (lane == 0) store16(out + len, tag, tag_aligned);

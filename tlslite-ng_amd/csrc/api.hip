@@ -556,6 +556,15 @@ int tg_key_create(int alg, const uint8_t* keys, size_t keylen, size_t nkeys, tg_
             aes.encrypt(rk, nr, zero, h);                     // H = E_K(0^128)
             build_ghash_tables(h, hk->ghash);
             for (int e = 0; e < 128 * (nr + 1); ++e) hk->bsmask[e] = tg::bs_mask_word(hk->rk, e);
+            {   // H^1 .. H^kHPow in normal order
+                uint32_t hn[4], p[4];
+                for (int w = 0; w < 4; ++w) hn[w] = tg::gcm_word_to_norm(le32(h + 4 * w));
+                for (int w = 0; w < 4; ++w) p[w] = hn[w];
+                for (int e = 0; e < tg::kHPow; ++e) {
+                    hk->hpow[e] = make_uint4(p[0], p[1], p[2], p[3]);
+                    tg::gf_mul_norm(p, hn, p);
+                }
+            }
             e = hipMalloc(&k->dev_key, sizeof(tg::GcmKeyDev));
             if (e == hipSuccess) e = hipMemcpy(k->dev_key, hk, sizeof(tg::GcmKeyDev), hipMemcpyHostToDevice);
             if (e != hipSuccess) rc = fail(TG_EHIP, "key upload: %s", hipGetErrorString(e));

@@ -25,7 +25,36 @@ struct GcmKeyDev {
     // bitsliced AES (aes_bs.h BsKeyMasks): plane mask (r, k, b) at (16 r + k) 8 + b
     // = 0 or ~0 by bit b of byte k of rk_r ^ (r ? 0x63 : 0) (see bs_mask_word)
     uint32_t bsmask[15 * 128];
+    uint4 hpow[1152];      // H^1 .. H^kHPow, normal order (gcm_wave_kernel)
 };
+
+// Powers of H for the wave-per-record kernel: hpow[e - 1] = H^e in normal
+// polynomial order (coefficient of x^i at bit i of the 128-bit value, word 0
+// first) for e = 1 .. kHPow.
+constexpr int kHPow = 1152;
+
+// a * b in GF(2^128) mod x^128 + x^7 + x^2 + x + 1, normal order, bitwise
+// (key setup only).
+__host__ __device__ inline void gf_mul_norm(const uint32_t a[4], const uint32_t b[4], uint32_t r[4]) {
+    uint32_t z[4] = {0, 0, 0, 0}, v[4] = {b[0], b[1], b[2], b[3]};
+    for (int i = 0; i < 128; ++i) {
+        if ((a[i >> 5] >> (i & 31)) & 1u)
+            for (int q = 0; q < 4; ++q) z[q] ^= v[q];
+        const uint32_t carry = v[3] >> 31;
+        v[3] = (v[3] << 1) | (v[2] >> 31);
+        v[2] = (v[2] << 1) | (v[1] >> 31);
+        v[1] = (v[1] << 1) | (v[0] >> 31);
+        v[0] = (v[0] << 1) ^ (carry ? 0x87u : 0u);
+    }
+    for (int q = 0; q < 4; ++q) r[q] = z[q];
+}
+
+// Normal-order word from a LE word of GCM block bytes: per-byte bit reversal.
+__host__ __device__ inline uint32_t gcm_word_to_norm(uint32_t w) {
+    uint32_t r = 0;
+    for (int k = 0; k < 32; ++k) r |= ((w >> k) & 1u) << ((k & ~7) + 7 - (k & 7));
+    return r;
+}
 
 // Entry e of GcmKeyDev::bsmask from the round-key words.
 __host__ __device__ inline uint32_t bs_mask_word(const uint32_t* rk, int e) {

@@ -357,6 +357,23 @@ __global__ void ghash_table_kernel(GcmKeyDev* key) {
     key->ghash[e] = make_uint4(w[0], w[1], w[2], w[3]);
 }
 
+// GcmKeyDev::hpow: thread e computes H^(e+1) by square and multiply from H,
+// which aes_setup_kernel parked in ghash[0] (the table kernel leaves entry 0
+// alone and the launcher zeroes it after this kernel, stream-ordered).
+__global__ void hpow_kernel(GcmKeyDev* key) {
+    const int e = blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= kHPow) return;
+    const uint4 hw = key->ghash[0];
+    const uint32_t hn[4] = {gcm_word_to_norm(hw.x), gcm_word_to_norm(hw.y), gcm_word_to_norm(hw.z),
+                            gcm_word_to_norm(hw.w)};
+    uint32_t r[4] = {1, 0, 0, 0}, x[4] = {hn[0], hn[1], hn[2], hn[3]};
+    for (uint32_t n = (uint32_t)e + 1; n; n >>= 1) {
+        if (n & 1) gf_mul_norm(r, x, r);
+        if (n > 1) gf_mul_norm(x, x, x);
+    }
+    key->hpow[e] = make_uint4(r[0], r[1], r[2], r[3]);
+}
+
 // GcmKeyDev::bsmask from the round keys (after aes_setup_kernel, layout 0).
 __global__ void bs_mask_kernel(GcmKeyDev* key) {
     const int e = blockIdx.x * blockDim.x + threadIdx.x;
@@ -402,6 +419,8 @@ int tg_launch_aes_setup(int keylen, int layout, const uint8_t* keys, uint64_t n,
     if (layout == 0) {
         tg::GcmKeyDev* k = static_cast<tg::GcmKeyDev*>(out);
         hipLaunchKernelGGL(tg::ghash_table_kernel, dim3(tg::kGhashEntries / 256), dim3(256), 0, s, k);
+        if (hipGetLastError() != hipSuccess) return TG_EHIP;
+        hipLaunchKernelGGL(tg::hpow_kernel, dim3((tg::kHPow + 255) / 256), dim3(256), 0, s, k);
         if (hipGetLastError() != hipSuccess) return TG_EHIP;
         hipLaunchKernelGGL(tg::bs_mask_kernel, dim3(15 * 128 / 256), dim3(256), 0, s, k);
         if (hipGetLastError() != hipSuccess) return TG_EHIP;
