@@ -64,7 +64,7 @@ def test_forced_kernel_vs_oracle(torch, tg, oracle_mod, alg, klen, var, value, a
 
 @pytest.mark.parametrize("alg,klen", [("aesgcm", 16), ("chacha", 32)])
 def test_auto_wave_per_record_batch(torch, tg, oracle_mod, alg, klen):
-    """A 2048-record batch (the largest that runs one record per wavefront)."""
+    """A 2048-record batch (four waves per record for AES-GCM, one for ChaCha)."""
     from batchpack import HostBatch, run_seal_open
     rng = np.random.default_rng(77 + klen)
     lens = list(rng.integers(0, 2049, 2048))
@@ -79,8 +79,10 @@ def test_auto_wave_per_record_batch(torch, tg, oracle_mod, alg, klen):
                                           ("aesgcm", 32, 29), ("chacha", 32, 29)])
 @pytest.mark.parametrize("align", [16, 1])
 def test_planned_mixed_batch(torch, tg, oracle_mod, alg, klen, keys, align):
-    """> 2048 records with per-record lengths run longest first (planner.hip):
-    every record must still land in its own output slot."""
+    """> 2048 records with per-record lengths on a lane-per-record kernel run
+    longest first (planner.hip): every record must still land in its own
+    output slot.  Single-key batches of this size run a wave per record by
+    default, so the lane kernel is forced for them."""
     from batchpack import HostBatch, run_seal_open
     rng = np.random.default_rng(1000 + klen + keys + align)
     lens = list(rng.integers(0, 3000, 5000)) + [16384, 16400, 0, 1] * 5
@@ -90,7 +92,44 @@ def test_planned_mixed_batch(torch, tg, oracle_mod, alg, klen, keys, align):
         obj = tg.HipAESGCM(bytearray(kb[0])) if alg == "aesgcm" else \
             tg.HipCHACHA20_POLY1305(bytearray(kb[0]))
         karr = np.frombuffer(kb[0], np.uint8)
+        env = ("TLSGPU_GCM_VARIANT", "5") if alg == "aesgcm" else ("TLSGPU_CHACHA_VARIANT", "4")
     else:
         obj = tg.KeyTable("chacha20-poly1305" if alg == "chacha" else "aesgcm", kb)
         karr = np.frombuffer(b"".join(kb), np.uint8).reshape(keys, klen)
-    run_seal_open(torch, tg, oracle_mod, hb, alg, karr, obj, tamper=(7, 2500, 5019))
+        env = ("TLSGPU_UNUSED", "0")
+    with _with_env(*env):
+        run_seal_open(torch, tg, oracle_mod, hb, alg, karr, obj, tamper=(7, 2500, 5019))
+
+
+@pytest.mark.parametrize("alg,klen", [("aesgcm", 16), ("chacha", 32)])
+def test_auto_mixed_batch_wave_path(torch, tg, oracle_mod, alg, klen):
+    """A mixed-length single-key batch above the old 2048-record limit runs a
+    wave per record without planning."""
+    from batchpack import HostBatch, run_seal_open
+    rng = np.random.default_rng(5 + klen)
+    lens = list(rng.integers(0, 3000, 6000)) + [16384, 16400, 0, 1] * 5
+    hb = HostBatch(lens, payload_seed=9, align=16, aad_mode="tls12")
+    key = rng.bytes(klen)
+    obj = tg.HipAESGCM(bytearray(key)) if alg == "aesgcm" else tg.HipCHACHA20_POLY1305(bytearray(key))
+    run_seal_open(torch, tg, oracle_mod, hb, alg, np.frombuffer(key, np.uint8), obj,
+                  tamper=(3, 4000, 6019))
+
+
+@pytest.mark.parametrize("alg,klen", [("aesgcm", 16), ("aesgcm", 32), ("chacha", 32)])
+@pytest.mark.parametrize("waves", ["1", "4", "16"])
+@pytest.mark.parametrize("align", [16, 1])
+def test_waves_per_record_forced(torch, tg, oracle_mod, alg, klen, waves, align):
+    """The wave-per-record kernels with one or four waves per record
+    (TLSGPU_WAVES_PER_RECORD; auto picks 16 / 4 / 1 by batch size):
+    the segment count changes every record's split point and H / r power."""
+    from batchpack import HostBatch, run_seal_open
+    rng = np.random.default_rng(int(waves) * 100 + klen + align)
+    lens = LENS * 3 + list(rng.integers(0, 16401, 60)) + [20000, 65000]
+    hb = HostBatch(lens, payload_seed=align + 40, align=align, aad_mode="random")
+    key = rng.bytes(klen)
+    obj = tg.HipAESGCM(bytearray(key)) if alg == "aesgcm" else tg.HipCHACHA20_POLY1305(bytearray(key))
+    var = "TLSGPU_GCM_VARIANT" if alg == "aesgcm" else "TLSGPU_CHACHA_VARIANT"
+    with _with_env(var, "6" if alg == "aesgcm" else "3"), \
+            _with_env("TLSGPU_WAVES_PER_RECORD", waves):
+        run_seal_open(torch, tg, oracle_mod, hb, alg, np.frombuffer(key, np.uint8), obj,
+                      tamper=(2, 50, len(lens) - 1))

@@ -760,18 +760,25 @@ int launch_bs(const GcmKeyDev* key, const tg_batch& b, hipStream_t s) {
 }
 
 // ---- wave-per-record kernel (small batches and the per-record calls) ----
-// One record per wavefront (the layout of the north star): the GHASH input
-// sequence AAD || C || length block, front-padded with zero blocks (neutral
-// for GHASH: y stays 0) to 64 B blocks, is split into 64 contiguous
-// segments of B blocks; lane l encrypts (T-table CTR, counters 2 + c) and
-// hashes its segment by Horner with the 8-bit GHASH tables in LDS.  Since
-// GHASH = sum_t X_t H^(64B - t), the lane's value is lifted by
-// H^(B (63 - l)) -- one table-free multiply by a power read from the key's
-// H^e table (GcmKeyDev::hpow) -- and the 64 lifted values are XOR-reduced
-// by shuffles.  A 16 KiB record is 17 blocks per lane instead of 1026 on
-// one lane.  Four records per 256-thread workgroup.
-constexpr int kWaveThreads = 256;
-constexpr size_t kWaveLds = 2 * 65536;   // GHASH tables at 0, Te0/Te2 copies at 64 KiB
+// One record per wavefront (the layout of the north star), or W waves per
+// record.  The GHASH input AAD || C || length block is front-padded with zero
+// blocks (neutral for GHASH: y stays 0) to P = 64 W Bw blocks; wave w of the
+// record takes the padded blocks [64 Bw w, 64 Bw (w + 1)) and lane l of it the
+// blocks 64 Bw w + 64 j + l (j < Bw), so every load and store instruction of
+// the wave covers 1 KiB of consecutive record bytes.  Lane l encrypts its
+// blocks (T-table CTR, counters 2 + c) and folds them by Horner with stride
+// H^64 (y <- y H^64 ^ X, the 8-bit tables of H^64 staged in LDS); since
+// GHASH = sum_t X_t H^(P - t), its value is then lifted by
+// H^(64 Bw (W - 1 - w) + 64 - l) -- one table-free multiply by a power from
+// the key's H^e table (GcmKeyDev::hpow) -- and the lifted values are
+// XOR-reduced by shuffles (and across the record's waves through LDS).
+constexpr int kWaveThreads = 1024;   // 16 waves share one LDS copy of the tables
+// GHASH tables at 0, Te0/Te2 copies at 64 KiB, then the per-wave partials
+// (16 x 16 B) and the per-record open verdicts (16 x 4 B).  The table lookups
+// use absolute LDS addresses, so this kernel must not declare static
+// __shared__ variables (they would move the dynamic region).
+constexpr size_t kWavePartBase = 2 * 65536;
+constexpr size_t kWaveLds = kWavePartBase + 16 * 16 + 16 * 4;
 
 __device__ __forceinline__ uint4 shfl_xor4(uint4 v, int m) {
     return make_uint4((uint32_t)__shfl_xor((int)v.x, m, 64), (uint32_t)__shfl_xor((int)v.y, m, 64),
@@ -794,19 +801,21 @@ __device__ __forceinline__ uint4 gf128_pow(uint4 x, uint32_t e) {
     return r;
 }
 
-template <int NR, bool OPEN>
-__global__ __launch_bounds__(kWaveThreads) void gcm_wave_kernel(const GcmKeyDev* __restrict__ key,
-                                                                tg_batch b) {
-    uint4* lds = g_lds;
-    for (int e = threadIdx.x; e < kGhashEntries; e += blockDim.x) lds[e] = key->ghash[e];
-    stage_te(reinterpret_cast<uint32_t*>(lds) + kTeBase / 4);
-    RkRegs<NR> rk;
-#pragma unroll
-    for (int k = 0; k < 4 * (NR + 1); ++k) rk.w[k] = key->rk[k];
-    __syncthreads();
-    const uint64_t i = (uint64_t)blockIdx.x * (kWaveThreads / 64) + (threadIdx.x >> 6);
-    if (i >= b.n) return;   // whole wave (uniform)
+// W waves per record (1, 4 or 16; 16 / W records per workgroup): more waves
+// per record for batches too small to fill the chip (the per-record calls).
+// (A persistent grid that stages the tables once per CU and loops over the
+// record groups measured slower: profiles/r01/v20_smallbatch.txt.)
+// All waves of a workgroup reach the barriers: a record slot past the end of
+// the batch recomputes the last record with its stores switched off.
+template <int NR, bool OPEN, int W>
+__device__ __forceinline__ void gcm_wave_record(const GcmKeyDev* __restrict__ key, const tg_batch& b,
+                                                const RkRegs<NR>& rk, uint64_t i, bool live,
+                                                uint32_t slot) {
+    constexpr uint32_t S = 64u * W;            // segments (threads) per record
+    uint4* s_part = g_lds + kWavePartBase / 16;
+    uint32_t* s_diff = reinterpret_cast<uint32_t*>(g_lds + kWavePartBase / 16 + 16);
     const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t seg = threadIdx.x & (S - 1u);
     const uint32_t lane4 = ((lane & 31u) << 2) | kTeBase;
     const uint8_t* in = rec_in(b, i);
     uint8_t* out = rec_out(b, i);
@@ -818,10 +827,13 @@ __global__ __launch_bounds__(kWaveThreads) void gcm_wave_kernel(const GcmKeyDev*
     const CtrCache cc = ctr_cache<NR>(lane4, rk, nv);
     const uint32_t na = (alen + 15) >> 4, nc = (len + 15) >> 4, nfull = len >> 4, tail = len & 15;
     const uint32_t M = na + nc + 1;            // GHASH blocks (aesgcm.py:60-79)
-    const uint32_t B = (M + 63) >> 6, pad = 64 * B - M;
+    const uint32_t Bw = (M + S - 1) / S, pad = S * Bw - M;
+    const uint32_t wv = seg >> 6;              // the record's wave
     const uint64_t abits = (uint64_t)alen << 3, cbits = (uint64_t)len << 3;
     uint4 y = make_uint4(0, 0, 0, 0);
-    for (uint32_t t = lane * B; t < lane * B + B; ++t) {
+    for (uint32_t j = 0; j < Bw; ++j) {
+        if (j) y = gmul(y);                     // y H^64 (wave-uniform)
+        const uint32_t t = 64 * (Bw * wv + j) + lane;
         if (t < pad) continue;                  // leading zero blocks
         const uint32_t k = t - pad;
         uint4 x;
@@ -834,67 +846,114 @@ __global__ __launch_bounds__(kWaveThreads) void gcm_wave_kernel(const GcmKeyDev*
             if (c < nfull) {
                 const uint4 d = load16(in + 16 * c, aligned);
                 const uint4 ct = xor4(d, ks);
-                store16(out + 16 * c, ct, aligned);
+                if (live) store16(out + 16 * c, ct, aligned);
                 x = OPEN ? d : ct;
             } else {
                 const uint4 d = load_partial(in + 16 * c, tail);
                 const uint4 ct = mask_tail(xor4(d, ks), tail);
-                store_partial(out + 16 * c, ct, tail);
+                if (live) store_partial(out + 16 * c, ct, tail);
                 x = OPEN ? d : ct;
             }
         } else {                                // be64(8 alen) || be64(8 len) (aesgcm.py:64)
             x = make_uint4(bswap32((uint32_t)(abits >> 32)), bswap32((uint32_t)abits),
                            bswap32((uint32_t)(cbits >> 32)), bswap32((uint32_t)cbits));
         }
-        y = gmul(xor4(y, x));
+        y = xor4(y, x);
     }
-    // lift by H^(B (63 - lane)) and XOR-reduce the 64 lanes
+    // lift by H^(64 Bw (W - 1 - w) + 64 - l) and XOR-reduce
     uint4 yn = norm4(y);
-    const uint32_t e = B * (63u - lane);
-    if (e && (y.x | y.y | y.z | y.w)) {
-        const uint4 hp = e <= (uint32_t)kHPow ? key->hpow[e - 1]
-                                              : gf128_pow(key->hpow[0], e);
+    if (y.x | y.y | y.z | y.w) {
+        const uint32_t e = 64 * Bw * (W - 1 - wv) + 64 - lane;
+        const uint4 hp = e <= (uint32_t)kHPow ? key->hpow[e - 1] : gf128_pow(key->hpow[0], e);
         yn = gf128_mul(yn, hp);
     }
 #pragma unroll
     for (int m = 1; m < 64; m <<= 1) yn = xor4(yn, shfl_xor4(yn, m));
+    if (W > 1) {
+        if (lane == 0) s_part[threadIdx.x >> 6] = yn;
+        __syncthreads();
+        yn = s_part[slot * W];
+#pragma unroll
+        for (int w = 1; w < W; ++w) yn = xor4(yn, s_part[slot * W + w]);
+    }
     // tag = GHASH ^ E_K(J0) (aesgcm.py:112-122)
     const uint4 mask = aes_ctr<NR>(lane4, rk, cc, 1u);
     const uint4 tag = xor4(norm4(yn), mask);
     const bool tag_aligned = aligned && tail == 0;
     if (!OPEN) {
-        if (lane == 0) store16(out + len, tag, tag_aligned);
+        if (seg == 0 && live) store16(out + len, tag, tag_aligned);
         return;
     }
     // open: compare (aesgcm.py:148-149); a rejected record's plaintext is zeroed
     uint32_t diff = 0;
-    if (lane == 0) {
+    if (seg == 0) {
         const uint4 exp = load16(in + len, tag_aligned);
         diff = (exp.x ^ tag.x) | (exp.y ^ tag.y) | (exp.z ^ tag.z) | (exp.w ^ tag.w);
-        if (b.status) b.status[i] = diff == 0;
+        if (b.status && live) b.status[i] = diff == 0;
+        if (W > 1) s_diff[slot] = diff;
     }
-    diff = (uint32_t)__shfl((int)diff, 0, 64);
+    if (W > 1) {
+        __syncthreads();
+        diff = live ? s_diff[slot] : 0;
+    } else {
+        diff = (uint32_t)__shfl((int)diff, 0, 64);
+    }
     if (diff) {
         const uint4 z = make_uint4(0, 0, 0, 0);
-        for (uint32_t c = lane; c < nfull; c += 64) store16(out + 16 * c, z, aligned);
-        if (tail && lane == 0) store_partial(out + 16 * nfull, z, tail);
+        for (uint32_t c = seg; c < nfull; c += S) store16(out + 16 * c, z, aligned);
+        if (tail && seg == 0) store_partial(out + 16 * nfull, z, tail);
     }
 }
 
-template <int NR, bool OPEN>
-int launch_wave(const GcmKeyDev* key, const tg_batch& b, hipStream_t s) {
+template <int NR, bool OPEN, int W>
+__global__ __launch_bounds__(kWaveThreads) void gcm_wave_kernel(const GcmKeyDev* __restrict__ key,
+                                                                tg_batch b) {
+    constexpr uint32_t R = kWaveThreads / (64u * W);   // records per group
+    for (int e = threadIdx.x; e < kGhashEntries; e += blockDim.x) g_lds[e] = key->ghash64[e];
+    stage_te(reinterpret_cast<uint32_t*>(g_lds) + kTeBase / 4);
+    RkRegs<NR> rk;
+#pragma unroll
+    for (int k = 0; k < 4 * (NR + 1); ++k) rk.w[k] = key->rk[k];
+    __syncthreads();
+    const uint32_t slot = threadIdx.x / (64u * W);
+    const uint64_t i0 = (uint64_t)blockIdx.x * R + slot;
+    const bool live = i0 < b.n;
+    if (W == 1 && !live) return;             // whole wave; no barriers for W = 1
+    gcm_wave_record<NR, OPEN, W>(key, b, rk, live ? i0 : b.n - 1, live, slot);
+}
+
+// Waves per record: enough for n * W waves to give each CU a 16-wave
+// workgroup (profiles/r01/v21_smallbatch.txt).
+int waves_per_record(uint64_t n) {
+    const char* env = getenv("TLSGPU_WAVES_PER_RECORD");
+    if (env) return atoi(env);
+    return n <= 256 ? 16 : n <= 2048 ? 4 : 1;
+}
+
+template <int NR, bool OPEN, int W>
+int launch_wave_w(const GcmKeyDev* key, const tg_batch& b, hipStream_t s) {
     static bool attr_set = false;
     if (!attr_set) {
-        if (hipFuncSetAttribute((const void*)gcm_wave_kernel<NR, OPEN>,
+        if (hipFuncSetAttribute((const void*)gcm_wave_kernel<NR, OPEN, W>,
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)kWaveLds) != hipSuccess)
             return TG_EHIP;
         attr_set = true;
     }
-    const uint64_t groups = (b.n + kWaveThreads / 64 - 1) / (kWaveThreads / 64);   // a wave per record
+    constexpr uint64_t per_group = kWaveThreads / (64 * W);
+    const uint64_t groups = (b.n + per_group - 1) / per_group;
     if (groups > 0x7fffffffull) return TG_EINVAL;
-    hipLaunchKernelGGL((gcm_wave_kernel<NR, OPEN>), dim3((unsigned)groups), dim3(kWaveThreads), kWaveLds,
-                       s, key, b);
+    hipLaunchKernelGGL((gcm_wave_kernel<NR, OPEN, W>), dim3((unsigned)groups), dim3(kWaveThreads),
+                       kWaveLds, s, key, b);
     return hipGetLastError() == hipSuccess ? TG_OK : TG_EHIP;
+}
+
+template <int NR, bool OPEN>
+int launch_wave(const GcmKeyDev* key, const tg_batch& b, hipStream_t s) {
+    switch (waves_per_record(b.n)) {
+        case 16: return launch_wave_w<NR, OPEN, 16>(key, b, s);
+        case 4: return launch_wave_w<NR, OPEN, 4>(key, b, s);
+        default: return launch_wave_w<NR, OPEN, 1>(key, b, s);
+    }
 }
 
 // Key-table kernel (many sessions per batch, BASELINE config 4): lane i uses
@@ -991,10 +1050,12 @@ int launch_v(const GcmKeyDev* key, const tg_batch& b, hipStream_t s, const uint3
 //   4          the bitsliced kernel (gcm_bs_kernel);
 //   6          the wave-per-record kernel (gcm_wave_kernel), which is also what
 //              batches of at most kWaveMaxRecords records use.
-// Up to this many records a batch runs one record per wavefront: below a
-// few thousand records a lane per record leaves most of the GPU idle while
-// one lane walks a whole record (profiles/r01/v11_latency_wave_per_record.txt).
-constexpr uint64_t kWaveMaxRecords = 2048;
+// Up to this many records a batch runs one record per wavefront: a lane per
+// record leaves most of the GPU idle while one lane walks a whole record
+// until the batch fills every lane slot of the chip; at 16 KiB the two
+// kernels meet at 2^18 records (profiles/r01/v21_smallbatch.txt), and the
+// wave kernel needs no length planning for mixed batches.
+constexpr uint64_t kWaveMaxRecords = 262144;
 
 int variant() {
     const char* e = getenv("TLSGPU_GCM_VARIANT");
@@ -1014,6 +1075,11 @@ int launch(const GcmKeyDev* key, const tg_batch& b, hipStream_t s, const uint32_
             if (b.n <= kWaveMaxRecords) return launch_wave<NR, OPEN>(key, b, s);
             return launch_v<NR, OPEN, 4, 1024, 0>(key, b, s, order);
     }
+}
+
+bool wave_path(uint64_t n) {
+    const int v = variant();
+    return v == 6 || (v == 0 && n <= kWaveMaxRecords);
 }
 
 template <int NR, bool OPEN>
@@ -1054,6 +1120,8 @@ int tg_launch_gcm_table(const tg::GcmTableKey* keys, int rounds, const tg_batch&
                     : tg::launch_table<14, false>(keys, b, s, order);
     return TG_EINVAL;
 }
+
+bool tg_gcm_wave_path(uint64_t n) { return tg::wave_path(n); }
 
 int tg_launch_gcm(const tg::GcmKeyDev* key, int rounds, const tg_batch& b, bool open,
                   hipStream_t s, const uint32_t* order) {

@@ -202,9 +202,10 @@ size_t dev_key_bytes(const tg_key* k) {
     return k->nkeys > 1 ? sizeof(tg::GcmTableKey) * k->nkeys : sizeof(tg::GcmKeyDev);
 }
 
-// Batches large enough for the lane-per-record kernels with per-record
-// lengths run longest first (planner.hip): a wave then holds records of
-// nearly one length instead of idling behind its longest.
+// Batches that run a lane-per-record kernel (many keys, or more records than
+// the wave-per-record kernels take) with per-record lengths run longest
+// first (planner.hip): a wave then holds records of nearly one length instead
+// of idling behind its longest.
 constexpr uint64_t kPlanMinRecords = 2049;
 
 // The order and the sort's scratch are allocated stream-ordered on the
@@ -214,7 +215,10 @@ int launch_kernels(tg_key* k, const tg_batch& b, bool open, hipStream_t s, const
 
 int launch(tg_key* k, const tg_batch& b, bool open, hipStream_t s) {
     const char* e = getenv("TLSGPU_NO_PLAN");
-    if (!b.len || b.n < kPlanMinRecords || is_ccm(k->alg) || b.n > 0xffffffffull || (e && atoi(e)))
+    const bool wave = k->nkeys == 1 && ((k->alg == TG_AES_GCM && tg_gcm_wave_path(b.n)) ||
+                                        (k->alg == TG_CHACHA20_POLY1305 && tg_chacha_wave_path(b.n)));
+    if (!b.len || b.n < kPlanMinRecords || wave || is_ccm(k->alg) || b.n > 0xffffffffull ||
+        (e && atoi(e)))
         return launch_kernels(k, b, open, s, nullptr);
     size_t scratch = 0;
     int rc = tg_length_order(b.len, b.n, nullptr, nullptr, &scratch, s);
@@ -564,6 +568,15 @@ int tg_key_create(int alg, const uint8_t* keys, size_t keylen, size_t nkeys, tg_
                     hk->hpow[e] = make_uint4(p[0], p[1], p[2], p[3]);
                     tg::gf_mul_norm(p, hn, p);
                 }
+            }
+            {   // the tables of H^64 (byte layout of hpow[63])
+                uint8_t h64[16];
+                const uint32_t pw[4] = {hk->hpow[63].x, hk->hpow[63].y, hk->hpow[63].z, hk->hpow[63].w};
+                for (int w = 0; w < 4; ++w) {
+                    const uint32_t v = tg::gcm_word_to_norm(pw[w]);
+                    for (int q = 0; q < 4; ++q) h64[4 * w + q] = (uint8_t)(v >> (8 * q));
+                }
+                build_ghash_tables(h64, hk->ghash64);
             }
             e = hipMalloc(&k->dev_key, sizeof(tg::GcmKeyDev));
             if (e == hipSuccess) e = hipMemcpy(k->dev_key, hk, sizeof(tg::GcmKeyDev), hipMemcpyHostToDevice);

@@ -341,13 +341,14 @@ __global__ __launch_bounds__(kChachaThreads, MINW) void chacha_kernel(
 }
 
 // ---- wave-per-record kernel (small batches and the per-record calls) ----
-// One record per wavefront: lane l takes the payload ChaCha blocks
-// [l Q, (l+1) Q) (counters 1 + q) and runs Poly1305's Horner over its
-// ciphertext 16-byte blocks; since acc = sum_k m_k r^(M-k) over the M
-// blocks of mac_data, each lane's partial result is lifted by
-// r^(blocks after its segment) (square and multiply in the same 26-bit limbs)
-// and the 64 partials are summed by a shuffle tree.  Lane 0 adds the AAD
-// blocks (lifted by r^(nc+1)) and the length block (times r).
+// One record per wavefront (or W waves, S = 64 W threads): thread t takes the
+// payload ChaCha blocks t, t + S, t + 2S, ... (counters 1 + q) and runs
+// Poly1305's Horner over its ciphertext 16-byte blocks, multiplying by
+// r^(4S - 4) across the gaps; since acc = sum_k m_k r^(M-k) over the M blocks
+// of mac_data, each thread's value is lifted by r^(blocks after its last one)
+// (square and multiply in the same 26-bit limbs) and the partials are summed
+// by a shuffle tree (and across the record's waves through LDS).  Thread 0
+// adds the AAD blocks (lifted by r^(nc+1)) and the length block (times r).
 struct F5 {
     uint32_t h0, h1, h2, h3, h4;
 };
@@ -402,12 +403,21 @@ __device__ __forceinline__ F5 fshfl_xor(const F5& v, int m) {
               (uint32_t)__shfl_xor((int)v.h4, m, 64)};
 }
 
-template <bool OPEN>
-__global__ __launch_bounds__(256) void chacha_wave_kernel(const ChachaKeyDev* __restrict__ keys,
-                                                          tg_batch b) {
-    const uint64_t i = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6);   // a wave per record
-    if (i >= b.n) return;   // whole wave (uniform)
-    const uint32_t lane = threadIdx.x & 63u;
+// W waves per record: W = 1 four records per 256-thread workgroup, W = 4 / 16
+// one record per 256 / 1024-thread workgroup (batches that leave CUs idle,
+// the per-record calls).
+template <int W>
+constexpr int chacha_wave_threads() { return W == 16 ? 1024 : 256; }
+
+template <bool OPEN, int W>
+__global__ __launch_bounds__(chacha_wave_threads<W>()) void chacha_wave_kernel(
+    const ChachaKeyDev* __restrict__ keys, tg_batch b) {
+    constexpr uint32_t S = 64u * W;            // segments (threads) per record
+    __shared__ F5 s_part[W];
+    __shared__ uint32_t s_diff;
+    const uint64_t i = (uint64_t)blockIdx.x * (chacha_wave_threads<W>() / S) + (threadIdx.x / S);
+    if (i >= b.n) return;   // whole record group (uniform)
+    const uint32_t lane = threadIdx.x & (S - 1u);
     uint32_t k[8];
 #pragma unroll
     for (int w = 0; w < 8; ++w) k[w] = keys->k[w];
@@ -426,9 +436,19 @@ __global__ __launch_bounds__(256) void chacha_wave_kernel(const ChachaKeyDev* __
     }
     const F5 r = {p.r0, p.r1, p.r2, p.r3, p.r4};
     const uint32_t nc = (len + 15) >> 4, nf = len >> 4, tail = len & 15;
-    const uint32_t nq = (len + 63) >> 6, Q = (nq + 63) >> 6;
-    const uint32_t q0 = lane * Q, q1 = q0 + Q < nq ? q0 + Q : nq;
-    for (uint32_t q = q0; q < q1; ++q) {            // chacha20_poly1305.py:58-63
+    const uint32_t nq = (len + 63) >> 6;
+    // thread seg takes the ChaCha blocks q = seg + S j, so each load / store
+    // instruction of a wave covers 4 KiB of consecutive bytes; between two of
+    // its blocks the Horner value skips the other threads' 4 (S - 1) Poly1305
+    // blocks: h <- h r^(4S - 4)
+    F5 rgap = {0, 0, 0, 0, 0};
+    uint32_t cb = 0;                                 // end of the thread's last block
+    for (uint32_t q = lane; q < nq; q += S) {        // chacha20_poly1305.py:58-63
+        if (q != lane) {
+            if (q == lane + S) rgap = fpow(r, 4 * S - 4);   // only threads with a gap
+            const F5 h = fmul(F5{p.h0, p.h1, p.h2, p.h3, p.h4}, rgap);
+            p.h0 = h.h0; p.h1 = h.h1; p.h2 = h.h2; p.h3 = h.h3; p.h4 = h.h4;
+        }
         uint32_t ks[16];
         chacha_block(k, 1 + q, nv.x, nv.y, nv.z, ks);
 #pragma unroll
@@ -447,10 +467,11 @@ __global__ __launch_bounds__(256) void chacha_wave_kernel(const ChachaKeyDev* __
                 poly_block(p, OPEN ? d : ct);
             }
         }
+        cb = 4 * q + 4 < nc ? 4 * q + 4 : nc;
     }
-    // lift the segment: acc_seg * r^(blocks after it, incl. the length block)
-    const uint32_t cb = 4 * q1 < nc ? 4 * q1 : nc;
-    F5 z = fmul(F5{p.h0, p.h1, p.h2, p.h3, p.h4}, fpow(r, nc - cb + 1));
+    // lift: h r^(blocks after the thread's last one, incl. the length block)
+    F5 z = F5{p.h0, p.h1, p.h2, p.h3, p.h4};
+    if (cb) z = fmul(z, fpow(r, nc - cb + 1));
     if (lane == 0) {
         Poly pa = p;                                 // the AAD (mac_data starts with it)
         pa.h0 = pa.h1 = pa.h2 = pa.h3 = pa.h4 = 0;
@@ -466,6 +487,13 @@ __global__ __launch_bounds__(256) void chacha_wave_kernel(const ChachaKeyDev* __
     }
 #pragma unroll
     for (int m = 1; m < 64; m <<= 1) z = fnorm_add(z, fshfl_xor(z, m));
+    if (W > 1) {
+        if ((lane & 63u) == 0) s_part[lane >> 6] = z;
+        __syncthreads();
+        z = s_part[0];
+#pragma unroll
+        for (int w = 1; w < W; ++w) z = fnorm_add(z, s_part[w]);
+    }
     p.h0 = z.h0; p.h1 = z.h1; p.h2 = z.h2; p.h3 = z.h3; p.h4 = z.h4;
     const uint4 tag = poly_finish(p);                // poly1305.py:47-48
     const bool tag_aligned = aligned && (len & 15) == 0;
@@ -478,18 +506,25 @@ __global__ __launch_bounds__(256) void chacha_wave_kernel(const ChachaKeyDev* __
         const uint4 exp = load16(in + len, tag_aligned);
         diff = (exp.x ^ tag.x) | (exp.y ^ tag.y) | (exp.z ^ tag.z) | (exp.w ^ tag.w);
         if (b.status) b.status[i] = diff == 0;
+        if (W > 1) s_diff = diff;
     }
-    diff = (uint32_t)__shfl((int)diff, 0, 64);
+    if (W > 1) {
+        __syncthreads();
+        diff = s_diff;
+    } else {
+        diff = (uint32_t)__shfl((int)diff, 0, 64);
+    }
     if (diff) {                                      // chacha20_poly1305.py:90-91
         const uint4 zz = make_uint4(0, 0, 0, 0);
-        for (uint32_t c = lane; c < nf; c += 64) store16(out + 16 * c, zz, aligned);
+        for (uint32_t c = lane; c < nf; c += S) store16(out + 16 * c, zz, aligned);
         if (tail && lane == 0) store_partial(out + 16 * nf, zz, tail);
     }
 }
 
 // Up to this many records a batch runs one record per wavefront (see the
-// GCM launcher; profiles/r01/v11_latency_wave_per_record.txt).
-constexpr uint64_t kWaveMaxRecords = 2048;
+// GCM launcher; at 16 KiB the kernels meet between 2^15 and 2^16 records:
+// profiles/r01/v21_smallbatch.txt).
+constexpr uint64_t kWaveMaxRecords = 49152;
 
 template <bool OPEN, bool MULTIKEY, int MINW>
 int launch_w(const ChachaKeyDev* keys, const tg_batch& b, hipStream_t s, const uint32_t* order) {
@@ -508,13 +543,29 @@ int chacha_variant() {
     return e ? atoi(e) : 0;
 }
 
+bool wave_path(uint64_t n) {
+    const int v = chacha_variant();
+    return v == 3 || (v == 0 && n <= kWaveMaxRecords);
+}
+
 template <bool OPEN, bool MULTIKEY>
 int launch(const ChachaKeyDev* keys, const tg_batch& b, hipStream_t s, const uint32_t* order) {
     const int v = chacha_variant();
-    if (!MULTIKEY && (v == 3 || (v == 0 && b.n <= kWaveMaxRecords))) {
-        const uint64_t groups = (b.n + 3) / 4;
+    if (!MULTIKEY && wave_path(b.n)) {
+        // waves per record as in the GCM launcher (aes_gcm.hip waves_per_record)
+        const char* env = getenv("TLSGPU_WAVES_PER_RECORD");
+        const int w = env ? atoi(env) : b.n <= 512 ? 4 : 1;   // profiles/r01/v21_smallbatch.txt
+        const uint64_t groups = w == 1 ? (b.n + 3) / 4 : b.n;
         if (groups > 0x7fffffffull) return TG_EINVAL;
-        hipLaunchKernelGGL((chacha_wave_kernel<OPEN>), dim3((unsigned)groups), dim3(256), 0, s, keys, b);
+        if (w == 16)
+            hipLaunchKernelGGL((chacha_wave_kernel<OPEN, 16>), dim3((unsigned)groups), dim3(1024), 0,
+                               s, keys, b);
+        else if (w == 4)
+            hipLaunchKernelGGL((chacha_wave_kernel<OPEN, 4>), dim3((unsigned)groups), dim3(256), 0, s,
+                               keys, b);
+        else
+            hipLaunchKernelGGL((chacha_wave_kernel<OPEN, 1>), dim3((unsigned)groups), dim3(256), 0, s,
+                               keys, b);
         return hipGetLastError() == hipSuccess ? TG_OK : TG_EHIP;
     }
     switch (v) {
@@ -546,6 +597,8 @@ __global__ void nonce_kernel(int mode, uint4 iv, uint64_t seq0, uint64_t n, uint
 
 }  // namespace
 }  // namespace tg
+
+bool tg_chacha_wave_path(uint64_t n) { return tg::wave_path(n); }
 
 int tg_launch_chacha(const tg::ChachaKeyDev* keys, const tg_batch& b, bool open, hipStream_t s,
                      const uint32_t* order) {

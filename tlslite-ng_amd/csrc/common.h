@@ -25,13 +25,14 @@ struct GcmKeyDev {
     // bitsliced AES (aes_bs.h BsKeyMasks): plane mask (r, k, b) at (16 r + k) 8 + b
     // = 0 or ~0 by bit b of byte k of rk_r ^ (r ? 0x63 : 0) (see bs_mask_word)
     uint32_t bsmask[15 * 128];
-    uint4 hpow[1152];      // H^1 .. H^kHPow, normal order (gcm_wave_kernel)
+    uint4 hpow[2048];      // H^1 .. H^kHPow, normal order (gcm_wave_kernel)
+    uint4 ghash64[kGhashEntries];   // the 8-bit tables of H^64 (gcm_wave_kernel's stride)
 };
 
 // Powers of H for the wave-per-record kernel: hpow[e - 1] = H^e in normal
 // polynomial order (coefficient of x^i at bit i of the 128-bit value, word 0
 // first) for e = 1 .. kHPow.
-constexpr int kHPow = 1152;
+constexpr int kHPow = 2048;
 
 // a * b in GF(2^128) mod x^128 + x^7 + x^2 + x + 1, normal order, bitwise
 // (key setup only).
@@ -186,6 +187,10 @@ int tg_length_order(const uint32_t* len, uint64_t n, uint32_t* order, void* scra
                     hipStream_t s);
 int tg_launch_ccm(const tg::AesKeyDev* keys, bool table, int rounds, int taglen,
                   const tg_batch& b, bool open, hipStream_t s);
+// Whether a single-key batch of n records runs the wave-per-record kernel
+// (no length planning needed then).
+bool tg_gcm_wave_path(uint64_t n);
+bool tg_chacha_wave_path(uint64_t n);
 int tg_launch_chacha(const tg::ChachaKeyDev* keys, const tg_batch& b, bool open, hipStream_t s,
                      const uint32_t* order = nullptr);
 int tg_launch_records_prep(const tg_records& r, bool seal, bool aes, int taglen,

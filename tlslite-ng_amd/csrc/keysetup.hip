@@ -322,12 +322,8 @@ __global__ void aes_setup_kernel(const uint8_t* __restrict__ keys, uint64_t n, v
 // block byte layout (api.hip build_ghash_tables; aesgcm.py:8-14 bit order).
 // Entry (0, 0) = 0 holds H on entry and is left alone here (every thread reads
 // it); the launcher zeroes it afterwards, stream-ordered.
-__global__ void ghash_table_kernel(GcmKeyDev* key) {
-    const int e = blockIdx.x * blockDim.x + threadIdx.x;   // entry j * 256 + b
-    if (e == 0 || e >= kGhashEntries) return;
-    const uint4 hw = key->ghash[0];                         // H as LE words of its bytes
+__device__ __forceinline__ uint4 ghash_table_entry(const uint32_t hv[4], int e) {
     const int j = e >> 8, b = e & 255;
-    const uint32_t hv[4] = {hw.x, hw.y, hw.z, hw.w};
     uint64_t hi = 0, lo = 0;
 #pragma unroll
     for (int k = 0; k < 8; ++k) hi = (hi << 8) | ((hv[k >> 2] >> (8 * (k & 3))) & 0xff);
@@ -354,7 +350,25 @@ __global__ void ghash_table_kernel(GcmKeyDev* key) {
         for (int k = 0; k < 4; ++k) v |= (uint32_t)((half >> (sh - 8 * k)) & 0xff) << (8 * k);
         w[q] = v;
     }
-    key->ghash[e] = make_uint4(w[0], w[1], w[2], w[3]);
+    return make_uint4(w[0], w[1], w[2], w[3]);
+}
+
+__global__ void ghash_table_kernel(GcmKeyDev* key) {
+    const int e = blockIdx.x * blockDim.x + threadIdx.x;   // entry j * 256 + b
+    if (e == 0 || e >= kGhashEntries) return;
+    const uint4 hw = key->ghash[0];                         // H as LE words of its bytes
+    const uint32_t hv[4] = {hw.x, hw.y, hw.z, hw.w};
+    key->ghash[e] = ghash_table_entry(hv, e);
+}
+
+// GcmKeyDev::ghash64: the same tables for H^64 (after hpow_kernel).
+__global__ void ghash64_table_kernel(GcmKeyDev* key) {
+    const int e = blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= kGhashEntries) return;
+    const uint4 p = key->hpow[63];                          // normal order -> byte layout
+    const uint32_t hv[4] = {gcm_word_to_norm(p.x), gcm_word_to_norm(p.y), gcm_word_to_norm(p.z),
+                            gcm_word_to_norm(p.w)};
+    key->ghash64[e] = ghash_table_entry(hv, e);
 }
 
 // GcmKeyDev::hpow: thread e computes H^(e+1) by square and multiply from H,
@@ -421,6 +435,8 @@ int tg_launch_aes_setup(int keylen, int layout, const uint8_t* keys, uint64_t n,
         hipLaunchKernelGGL(tg::ghash_table_kernel, dim3(tg::kGhashEntries / 256), dim3(256), 0, s, k);
         if (hipGetLastError() != hipSuccess) return TG_EHIP;
         hipLaunchKernelGGL(tg::hpow_kernel, dim3((tg::kHPow + 255) / 256), dim3(256), 0, s, k);
+        if (hipGetLastError() != hipSuccess) return TG_EHIP;
+        hipLaunchKernelGGL(tg::ghash64_table_kernel, dim3(tg::kGhashEntries / 256), dim3(256), 0, s, k);
         if (hipGetLastError() != hipSuccess) return TG_EHIP;
         hipLaunchKernelGGL(tg::bs_mask_kernel, dim3(15 * 128 / 256), dim3(256), 0, s, k);
         if (hipGetLastError() != hipSuccess) return TG_EHIP;
