@@ -96,7 +96,7 @@ def test_planned_mixed_batch(torch, tg, oracle_mod, alg, klen, keys, align):
     else:
         obj = tg.KeyTable("chacha20-poly1305" if alg == "chacha" else "aesgcm", kb)
         karr = np.frombuffer(b"".join(kb), np.uint8).reshape(keys, klen)
-        env = ("TLSGPU_UNUSED", "0")
+        env = ("TLSGPU_GCM_TABLE_VARIANT", "0")   # AES: the lane kernel
     with _with_env(*env):
         run_seal_open(torch, tg, oracle_mod, hb, alg, karr, obj, tamper=(7, 2500, 5019))
 
@@ -133,3 +133,23 @@ def test_waves_per_record_forced(torch, tg, oracle_mod, alg, klen, waves, align)
             _with_env("TLSGPU_WAVES_PER_RECORD", waves):
         run_seal_open(torch, tg, oracle_mod, hb, alg, np.frombuffer(key, np.uint8), obj,
                       tamper=(2, 50, len(lens) - 1))
+
+
+@pytest.mark.parametrize("klen", [16, 32])
+@pytest.mark.parametrize("threads", ["512", "768", "1024"])
+@pytest.mark.parametrize("align", [16, 1])
+def test_key_table_wave_kernel(torch, tg, oracle_mod, klen, threads, align):
+    """Many keys, mixed lengths, one wave per record (gcm_table_wave_kernel,
+    key-table variant 5): round keys from the record's key, GHASH powers from
+    the key's precomputed table."""
+    from batchpack import HostBatch, run_seal_open
+    rng = np.random.default_rng(300 + klen + int(threads) + align)
+    lens = LENS * 4 + list(rng.integers(0, 16401, 300)) + [20000, 65000]
+    keys = 37
+    hb = HostBatch(lens, payload_seed=align + 77, align=align, aad_mode="random", key_count=keys)
+    kb = [rng.bytes(klen) for _ in range(keys)]
+    obj = tg.KeyTable("aesgcm", kb)
+    karr = np.frombuffer(b"".join(kb), np.uint8).reshape(keys, klen)
+    with _with_env("TLSGPU_GCM_TABLE_WAVE_THREADS", threads), \
+            _with_env("TLSGPU_GCM_TABLE_VARIANT", "5"):
+        run_seal_open(torch, tg, oracle_mod, hb, "aesgcm", karr, obj, tamper=(4, 100, len(lens) - 1))

@@ -1022,6 +1022,158 @@ int launch_table_v(const GcmTableKey* keys, const tg_batch& b, hipStream_t s, co
     return hipGetLastError() == hipSuccess ? TG_OK : TG_EHIP;
 }
 
+// Key-table wave-per-record kernel (many sessions, mixed lengths; BASELINE
+// config 4).  Wave w of the workgroup seals / opens record i with key
+// key_idx[i]: the index is wave-uniform, so the round keys are scalar loads
+// into SGPRs (no VGPRs, no LDS rows).  The layout is the single-key wave
+// kernel's with W = 1 (lane l takes blocks l, l + 64, ...: coalesced), but
+// GHASH is the table-free multiply: Horner with stride H^64 and one lift by
+// H^(64 - l), both read from the key's 64 precomputed powers
+// (hpow[64 k + e - 1] = H^e, built at key setup by table_hpow_kernel).
+// No length planning: a wave takes as long as its own record.
+template <int NR, bool OPEN>
+__device__ __forceinline__ void gcm_table_wave_record(const GcmTableKey* __restrict__ keys,
+                                                      const uint4* __restrict__ hpow,
+                                                      const tg_batch& b, uint64_t i, uint32_t lane) {
+    const uint32_t ki = (uint32_t)__builtin_amdgcn_readfirstlane((int)(b.key_idx ? b.key_idx[i] : 0u));
+    const GcmTableKey* kp = keys + ki;
+    RkRegs<NR> rk;   // wave-uniform: SGPRs
+#pragma unroll
+    for (int k = 0; k < 4 * (NR + 1); ++k) rk.w[k] = kp->rk[k];
+    const uint4* hp = hpow + 64ull * ki;
+    const uint4 h64 = hp[63];
+    const uint32_t lane4 = (lane & 31u) << 2;
+    const uint8_t* in = rec_in(b, i);
+    uint8_t* out = rec_out(b, i);
+    const uint32_t len = rec_len(b, i);
+    const uint8_t* ad = rec_aad(b, i);
+    const uint32_t alen = rec_aad_len(b, i);
+    const bool aligned = (((uintptr_t)in | (uintptr_t)out) & 15) == 0;
+    const uint4 nv = load_partial(b.nonce + 12 * i, 12);
+    const CtrCache cc = ctr_cache<NR>(lane4, rk, nv);
+    const uint32_t na = (alen + 15) >> 4, nc = (len + 15) >> 4, nfull = len >> 4, tail = len & 15;
+    const uint32_t M = na + nc + 1;            // GHASH blocks (aesgcm.py:60-79)
+    const uint32_t Bw = (M + 63) >> 6, pad = 64 * Bw - M;
+    const uint64_t abits = (uint64_t)alen << 3, cbits = (uint64_t)len << 3;
+    uint4 y = make_uint4(0, 0, 0, 0);          // normal order
+    for (uint32_t j = 0; j < Bw; ++j) {
+        if (j) y = gf128_mul(y, h64);           // y H^64 (wave-uniform)
+        const uint32_t t = 64 * j + lane;
+        if (t < pad) continue;                  // leading zero blocks
+        const uint32_t k = t - pad;
+        uint4 x;
+        if (k < na) {
+            const uint32_t m = alen - 16 * k < 16 ? alen - 16 * k : 16;
+            x = load_partial(ad + 16 * k, m);
+        } else if (k < na + nc) {               // CTR block c (python_aes.py:101-116)
+            const uint32_t c = k - na;
+            const uint4 ks = aes_ctr<NR>(lane4, rk, cc, 2u + c);
+            if (c < nfull) {
+                const uint4 d = load16(in + 16 * c, aligned);
+                const uint4 ct = xor4(d, ks);
+                store16(out + 16 * c, ct, aligned);
+                x = OPEN ? d : ct;
+            } else {
+                const uint4 d = load_partial(in + 16 * c, tail);
+                const uint4 ct = mask_tail(xor4(d, ks), tail);
+                store_partial(out + 16 * c, ct, tail);
+                x = OPEN ? d : ct;
+            }
+        } else {                                // be64(8 alen) || be64(8 len) (aesgcm.py:64)
+            x = make_uint4(bswap32((uint32_t)(abits >> 32)), bswap32((uint32_t)abits),
+                           bswap32((uint32_t)(cbits >> 32)), bswap32((uint32_t)cbits));
+        }
+        y = xor4(y, norm4(x));
+    }
+    if (y.x | y.y | y.z | y.w) y = gf128_mul(y, hp[63 - lane]);   // lift by H^(64 - l)
+#pragma unroll
+    for (int m = 1; m < 64; m <<= 1) y = xor4(y, shfl_xor4(y, m));
+    // tag = GHASH ^ E_K(J0) (aesgcm.py:112-122)
+    const uint4 tag = xor4(norm4(y), aes_ctr<NR>(lane4, rk, cc, 1u));
+    const bool tag_aligned = aligned && tail == 0;
+    if (!OPEN) {
+        if (lane == 0) store16(out + len, tag, tag_aligned);
+        return;
+    }
+    uint32_t diff = 0;                          // aesgcm.py:148-149
+    if (lane == 0) {
+        const uint4 exp = load16(in + len, tag_aligned);
+        diff = (exp.x ^ tag.x) | (exp.y ^ tag.y) | (exp.z ^ tag.z) | (exp.w ^ tag.w);
+        if (b.status) b.status[i] = diff == 0;
+    }
+    diff = (uint32_t)__shfl((int)diff, 0, 64);
+    if (diff) {
+        const uint4 z = make_uint4(0, 0, 0, 0);
+        for (uint32_t c = lane; c < nfull; c += 64) store16(out + 16 * c, z, aligned);
+        if (tail && lane == 0) store_partial(out + 16 * nfull, z, tail);
+    }
+}
+
+// A persistent grid (two workgroups per CU): wave g takes records g, g + G,
+// g + 2G, ... so a workgroup's waves finish together however the lengths mix
+// (one workgroup per record group would hold its LDS until its longest
+// record is done).
+template <int NR, bool OPEN, int kTwThreads>
+__global__ __launch_bounds__(kTwThreads) void gcm_table_wave_kernel(
+    const GcmTableKey* __restrict__ keys, const uint4* __restrict__ hpow, tg_batch b) {
+    stage_te(reinterpret_cast<uint32_t*>(g_lds));   // Te0/Te2 copies at LDS 0
+    __syncthreads();
+    const uint64_t G = (uint64_t)gridDim.x * (kTwThreads / 64);
+    const uint32_t wave = (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    for (uint64_t i = (uint64_t)blockIdx.x * (kTwThreads / 64) + wave; i < b.n; i += G)
+        gcm_table_wave_record<NR, OPEN>(keys, hpow, b, i, threadIdx.x & 63u);
+}
+
+// Threads per workgroup: two workgroups (2 x 64 KiB of T-tables) per CU.
+template <int NR, bool OPEN, int kTwThreads>
+int launch_table_wave_t(const GcmTableKey* keys, const uint4* hpow, const tg_batch& b,
+                        hipStream_t s) {
+    static bool attr_set = false;
+    if (!attr_set) {
+        if (hipFuncSetAttribute((const void*)gcm_table_wave_kernel<NR, OPEN, kTwThreads>,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, 65536) != hipSuccess)
+            return TG_EHIP;
+        attr_set = true;
+    }
+    const uint64_t groups = (b.n + kTwThreads / 64 - 1) / (kTwThreads / 64);
+    const uint64_t cap = 2ull * (uint64_t)device_cus();
+    hipLaunchKernelGGL((gcm_table_wave_kernel<NR, OPEN, kTwThreads>), dim3((unsigned)(groups < cap ? groups : cap)),
+                       dim3(kTwThreads), 65536, s, keys, hpow, b);
+    return hipGetLastError() == hipSuccess ? TG_OK : TG_EHIP;
+}
+
+template <int NR, bool OPEN>
+int launch_table_wave(const GcmTableKey* keys, const uint4* hpow, const tg_batch& b, hipStream_t s) {
+    const char* e = getenv("TLSGPU_GCM_TABLE_WAVE_THREADS");   // measurement
+    switch (e ? atoi(e) : 768) {
+        case 512: return launch_table_wave_t<NR, OPEN, 512>(keys, hpow, b, s);
+        case 1024: return launch_table_wave_t<NR, OPEN, 1024>(keys, hpow, b, s);
+        default: return launch_table_wave_t<NR, OPEN, 768>(keys, hpow, b, s);
+    }
+}
+
+// The key table's GHASH powers for gcm_table_wave_kernel: one wave per key,
+// lane l ends with H^(l + 1) (normal order); after the step with distance d
+// lanes [0, 2d) hold their powers (H^(l + 1) = H^(l + 1 - d) * H^d).
+__global__ __launch_bounds__(256) void table_hpow_kernel(const GcmTableKey* __restrict__ keys,
+                                                         uint64_t n, uint4* __restrict__ hpow) {
+    const uint64_t key = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (key >= n) return;
+    const int lane = threadIdx.x & 63;
+    const uint4 h = *reinterpret_cast<const uint4*>(keys[key].hn);
+    uint4 p = h;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint4 hd = make_uint4((uint32_t)__shfl((int)p.x, d - 1, 64), (uint32_t)__shfl((int)p.y, d - 1, 64),
+                                    (uint32_t)__shfl((int)p.z, d - 1, 64), (uint32_t)__shfl((int)p.w, d - 1, 64));
+        const int src = lane >= d ? lane - d : lane;
+        const uint4 q = make_uint4((uint32_t)__shfl((int)p.x, src, 64), (uint32_t)__shfl((int)p.y, src, 64),
+                                   (uint32_t)__shfl((int)p.z, src, 64), (uint32_t)__shfl((int)p.w, src, 64));
+        if (lane >= d && lane < 2 * d) p = gf128_mul(q, hd);
+    }
+    hpow[64 * key + lane] = p;
+}
+
 int table_variant() {
     const char* e = getenv("TLSGPU_GCM_TABLE_VARIANT");
     return e ? atoi(e) : 0;
@@ -1082,11 +1234,20 @@ bool wave_path(uint64_t n) {
     return v == 6 || (v == 0 && n <= kWaveMaxRecords);
 }
 
+bool table_wave_path(uint64_t n) {
+    (void)n;
+    return table_variant() == 5;
+}
+
 template <int NR, bool OPEN>
-int launch_table(const GcmTableKey* keys, const tg_batch& b, hipStream_t s, const uint32_t* order) {
-    // TLSGPU_GCM_TABLE_VARIANT (measurement): 0 = round keys in VGPRs, 768
-    // threads (config 4: 368 GiB/s); 2 = the same at 512 threads (346);
-    // 3 = at 1024 threads (217, spills); 9 = round keys in LDS rows (230).
+int launch_table(const GcmTableKey* keys, const uint4* hpow, const tg_batch& b, hipStream_t s,
+                 const uint32_t* order) {
+    // TLSGPU_GCM_TABLE_VARIANT (measurement): 0 = lane per record, round keys
+    // in VGPRs, 768 threads (config 4: 368 GiB/s); 2 = the same at 512 threads
+    // (346); 3 = at 1024 threads (217, spills); 9 = round keys in LDS rows
+    // (230); 5 = wave per record (gcm_table_wave_kernel: 358, both bound by the
+    // table-free GHASH multiply; profiles/r01/v24_c4_*.json).
+    if (table_wave_path(b.n) && hpow) return launch_table_wave<NR, OPEN>(keys, hpow, b, s);
     switch (table_variant()) {
         case 2: return launch_table_v<NR, OPEN, 512>(keys, b, s, order);
         case 3: return launch_table_v<NR, OPEN, 1024>(keys, b, s, order);
@@ -1110,14 +1271,23 @@ int launch_table(const GcmTableKey* keys, const tg_batch& b, hipStream_t s, cons
 }  // namespace
 }  // namespace tg
 
-int tg_launch_gcm_table(const tg::GcmTableKey* keys, int rounds, const tg_batch& b, bool open,
-                        hipStream_t s, const uint32_t* order) {
+bool tg_gcm_table_wave_path(uint64_t n) { return tg::table_wave_path(n); }
+
+int tg_launch_table_hpow(const tg::GcmTableKey* keys, uint64_t n, uint4* hpow, hipStream_t s) {
+    const uint64_t groups = (n + 3) / 4;
+    if (groups > 0x7fffffffull) return TG_EINVAL;
+    hipLaunchKernelGGL(tg::table_hpow_kernel, dim3((unsigned)groups), dim3(256), 0, s, keys, n, hpow);
+    return hipGetLastError() == hipSuccess ? TG_OK : TG_EHIP;
+}
+
+int tg_launch_gcm_table(const tg::GcmTableKey* keys, const uint4* hpow, int rounds,
+                        const tg_batch& b, bool open, hipStream_t s, const uint32_t* order) {
     if (rounds == 10)
-        return open ? tg::launch_table<10, true>(keys, b, s, order)
-                    : tg::launch_table<10, false>(keys, b, s, order);
+        return open ? tg::launch_table<10, true>(keys, hpow, b, s, order)
+                    : tg::launch_table<10, false>(keys, hpow, b, s, order);
     if (rounds == 14)
-        return open ? tg::launch_table<14, true>(keys, b, s, order)
-                    : tg::launch_table<14, false>(keys, b, s, order);
+        return open ? tg::launch_table<14, true>(keys, hpow, b, s, order)
+                    : tg::launch_table<14, false>(keys, hpow, b, s, order);
     return TG_EINVAL;
 }
 

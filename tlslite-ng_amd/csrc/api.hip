@@ -196,10 +196,19 @@ int ensure_stage(tg_key* k, size_t bytes) {
 
 bool is_ccm(int alg) { return alg == TG_AES_CCM || alg == TG_AES_CCM_8; }
 
+// A multi-key AES-GCM allocation: GcmTableKey[nkeys], then the 64 GHASH
+// powers of each key (gcm_table_wave_kernel).
+constexpr size_t kTableHpowBytes = 64 * sizeof(uint4);
+uint4* table_hpow(const tg_key* k) {
+    return reinterpret_cast<uint4*>(static_cast<uint8_t*>(k->dev_key) +
+                                    sizeof(tg::GcmTableKey) * k->nkeys);
+}
+
 size_t dev_key_bytes(const tg_key* k) {
     if (k->alg == TG_CHACHA20_POLY1305) return sizeof(tg::ChachaKeyDev) * k->nkeys;
     if (is_ccm(k->alg)) return sizeof(tg::AesKeyDev) * k->nkeys;
-    return k->nkeys > 1 ? sizeof(tg::GcmTableKey) * k->nkeys : sizeof(tg::GcmKeyDev);
+    return k->nkeys > 1 ? (sizeof(tg::GcmTableKey) + kTableHpowBytes) * k->nkeys
+                        : sizeof(tg::GcmKeyDev);
 }
 
 // Batches that run a lane-per-record kernel (many keys, or more records than
@@ -215,8 +224,9 @@ int launch_kernels(tg_key* k, const tg_batch& b, bool open, hipStream_t s, const
 
 int launch(tg_key* k, const tg_batch& b, bool open, hipStream_t s) {
     const char* e = getenv("TLSGPU_NO_PLAN");
-    const bool wave = k->nkeys == 1 && ((k->alg == TG_AES_GCM && tg_gcm_wave_path(b.n)) ||
-                                        (k->alg == TG_CHACHA20_POLY1305 && tg_chacha_wave_path(b.n)));
+    const bool wave = k->nkeys == 1 ? ((k->alg == TG_AES_GCM && tg_gcm_wave_path(b.n)) ||
+                                       (k->alg == TG_CHACHA20_POLY1305 && tg_chacha_wave_path(b.n)))
+                                    : k->alg == TG_AES_GCM && tg_gcm_table_wave_path(b.n);
     if (!b.len || b.n < kPlanMinRecords || wave || is_ccm(k->alg) || b.n > 0xffffffffull ||
         (e && atoi(e)))
         return launch_kernels(k, b, open, s, nullptr);
@@ -238,8 +248,8 @@ int launch_kernels(tg_key* k, const tg_batch& b, bool open, hipStream_t s, const
         return tg_launch_ccm(static_cast<const tg::AesKeyDev*>(k->dev_key), k->nkeys > 1,
                              k->rounds, k->taglen, b, open, s);
     if (k->alg == TG_AES_GCM && k->nkeys > 1)
-        return tg_launch_gcm_table(static_cast<const tg::GcmTableKey*>(k->dev_key), k->rounds, b,
-                                   open, s, order);
+        return tg_launch_gcm_table(static_cast<const tg::GcmTableKey*>(k->dev_key), table_hpow(k),
+                                   k->rounds, b, open, s, order);
     if (k->alg == TG_AES_GCM)
         return tg_launch_gcm(static_cast<const tg::GcmKeyDev*>(k->dev_key), k->rounds, b, open, s,
                              order);
@@ -540,9 +550,14 @@ int tg_key_create(int alg, const uint8_t* keys, size_t keylen, size_t nkeys, tg_
                 memset(rk, 0, sizeof(rk));
             }
             const size_t bytes = sizeof(tg::GcmTableKey) * nkeys;
-            e = hipMalloc(&k->dev_key, bytes);
+            e = hipMalloc(&k->dev_key, dev_key_bytes(k));
             if (e == hipSuccess) e = hipMemcpy(k->dev_key, hk, bytes, hipMemcpyHostToDevice);
             if (e != hipSuccess) rc = fail(TG_EHIP, "key upload: %s", hipGetErrorString(e));
+            if (!rc && tg_launch_table_hpow(static_cast<const tg::GcmTableKey*>(k->dev_key), nkeys,
+                                            table_hpow(k), nullptr))
+                rc = fail(TG_EHIP, "key powers launch failed");
+            if (!rc && (e = hipDeviceSynchronize()) != hipSuccess)
+                rc = fail(TG_EHIP, "key powers: %s", hipGetErrorString(e));
             memset(hk, 0, sizeof(tg::GcmTableKey) * nkeys);
             delete[] hk;
         }
@@ -624,6 +639,9 @@ int tg_key_create_device(int alg, const uint8_t* keys, size_t keylen, size_t nke
     } else {
         const int layout = is_ccm(alg) ? 2 : (nkeys > 1 ? 1 : 0);
         rc = tg_launch_aes_setup((int)keylen, layout, keys, nkeys, k->dev_key, st);
+        if (!rc && layout == 1)
+            rc = tg_launch_table_hpow(static_cast<const tg::GcmTableKey*>(k->dev_key), nkeys,
+                                      table_hpow(k), st);
         if (rc) rc = fail(rc, "key setup launch failed");
     }
     if (!rc && (e = hipStreamSynchronize(st)) != hipSuccess)

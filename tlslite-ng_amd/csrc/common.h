@@ -174,6 +174,22 @@ struct RecScratch {
     uint8_t* dummy;       // 32 zero bytes: AEAD input of publicly-invalid records
 };
 
+// Compute units of the current device (grid size of the persistent kernels),
+// looked up once per device.
+inline int device_cus() {
+    static int cache[64] = {0};
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) dev = 0;
+    if (!cache[dev]) {
+        int cus = 0;
+        if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+            cus <= 0)
+            cus = 256;
+        cache[dev] = cus;
+    }
+    return cache[dev];
+}
+
 }  // namespace tg
 
 // Launchers implemented in the kernel files (host side).
@@ -181,8 +197,13 @@ struct RecScratch {
 // t of a lane-per-record kernel handles record order[t].
 int tg_launch_gcm(const tg::GcmKeyDev* key, int rounds, const tg_batch& b, bool open,
                   hipStream_t s, const uint32_t* order = nullptr);
-int tg_launch_gcm_table(const tg::GcmTableKey* keys, int rounds, const tg_batch& b, bool open,
-                        hipStream_t s, const uint32_t* order = nullptr);
+// hpow: the key table's GHASH powers (tg_launch_table_hpow), or NULL for the
+// lane-per-record kernels only.
+int tg_launch_gcm_table(const tg::GcmTableKey* keys, const uint4* hpow, int rounds,
+                        const tg_batch& b, bool open, hipStream_t s, const uint32_t* order = nullptr);
+// hpow[64 k + e - 1] = H_k^e (normal order), e = 1..64, for the n keys.
+int tg_launch_table_hpow(const tg::GcmTableKey* keys, uint64_t n, uint4* hpow, hipStream_t s);
+bool tg_gcm_table_wave_path(uint64_t n);
 int tg_length_order(const uint32_t* len, uint64_t n, uint32_t* order, void* scratch, size_t* bytes,
                     hipStream_t s);
 int tg_launch_ccm(const tg::AesKeyDev* keys, bool table, int rounds, int taglen,
