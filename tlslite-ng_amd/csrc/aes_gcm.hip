@@ -915,7 +915,8 @@ __global__ __launch_bounds__(kWaveThreads) void gcm_wave_kernel(const GcmKeyDev*
 #pragma unroll
     for (int k = 0; k < 4 * (NR + 1); ++k) rk.w[k] = key->rk[k];
     __syncthreads();
-    const uint32_t slot = threadIdx.x / (64u * W);
+    // wave-uniform (readfirstlane): the record's fields become scalar loads
+    const uint32_t slot = (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x / (64u * W)));
     const uint64_t i0 = (uint64_t)blockIdx.x * R + slot;
     const bool live = i0 < b.n;
     if (W == 1 && !live) return;             // whole wave; no barriers for W = 1

@@ -415,7 +415,8 @@ __global__ __launch_bounds__(chacha_wave_threads<W>()) void chacha_wave_kernel(
     constexpr uint32_t S = 64u * W;            // segments (threads) per record
     __shared__ F5 s_part[W];
     __shared__ uint32_t s_diff;
-    const uint64_t i = (uint64_t)blockIdx.x * (chacha_wave_threads<W>() / S) + (threadIdx.x / S);
+    const uint64_t i = (uint64_t)blockIdx.x * (chacha_wave_threads<W>() / S) +
+                       (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x / S));   // wave-uniform
     if (i >= b.n) return;   // whole record group (uniform)
     const uint32_t lane = threadIdx.x & (S - 1u);
     uint32_t k[8];
