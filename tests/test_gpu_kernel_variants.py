@@ -42,8 +42,11 @@ LENS = [0, 1, 15, 16, 17, 63, 64, 65, 1000, 1024, 1040, 4095, 16383, 16384, 1638
 
 
 @pytest.mark.parametrize("alg,klen,var,value", [
-    ("aesgcm", 16, "TLSGPU_GCM_VARIANT", "5"),          # lane per record
+    ("aesgcm", 16, "TLSGPU_GCM_VARIANT", "5"),          # lane per record, full rounds
     ("aesgcm", 32, "TLSGPU_GCM_VARIANT", "5"),
+    ("aesgcm", 16, "TLSGPU_GCM_VARIANT", "7"),          # lane per record, counter windows
+    ("aesgcm", 32, "TLSGPU_GCM_VARIANT", "7"),
+    ("aesgcm", 16, "TLSGPU_GCM_VARIANT", "8"),          # windows, two blocks per group
     ("aesgcm", 16, "TLSGPU_GCM_VARIANT", "6"),          # wave per record
     ("aesgcm", 32, "TLSGPU_GCM_VARIANT", "6"),
     ("chacha", 32, "TLSGPU_CHACHA_VARIANT", "4"),       # lane per record
@@ -53,7 +56,8 @@ LENS = [0, 1, 15, 16, 17, 63, 64, 65, 1000, 1024, 1040, 4095, 16383, 16384, 1638
 def test_forced_kernel_vs_oracle(torch, tg, oracle_mod, alg, klen, var, value, align):
     from batchpack import HostBatch, run_seal_open
     rng = np.random.default_rng(hash((alg, klen, value, align)) & 0xffff)
-    lens = LENS * 5 + list(rng.integers(0, 16401, 120))
+    # + long records: many 256-counter windows (window-cache refreshes)
+    lens = LENS * 5 + list(rng.integers(0, 16401, 120)) + [65520, 65536, 70001]
     hb = HostBatch(lens, payload_seed=align + 21, align=align, aad_mode="random")
     key = rng.bytes(klen)
     obj = tg.HipAESGCM(bytearray(key)) if alg == "aesgcm" else tg.HipCHACHA20_POLY1305(bytearray(key))
@@ -92,7 +96,7 @@ def test_planned_mixed_batch(torch, tg, oracle_mod, alg, klen, keys, align):
         obj = tg.HipAESGCM(bytearray(kb[0])) if alg == "aesgcm" else \
             tg.HipCHACHA20_POLY1305(bytearray(kb[0]))
         karr = np.frombuffer(kb[0], np.uint8)
-        env = ("TLSGPU_GCM_VARIANT", "5") if alg == "aesgcm" else ("TLSGPU_CHACHA_VARIANT", "4")
+        env = ("TLSGPU_GCM_VARIANT", "7") if alg == "aesgcm" else ("TLSGPU_CHACHA_VARIANT", "4")
     else:
         obj = tg.KeyTable("chacha20-poly1305" if alg == "chacha" else "aesgcm", kb)
         karr = np.frombuffer(b"".join(kb), np.uint8).reshape(keys, klen)

@@ -270,16 +270,17 @@ struct GhashClmul {  // y kept in normal order; hn = H in normal order
 // SPLIT: a scheduling fence between the AES of group g+1 and the GHASH of
 // group g, so their register peaks do not add up (the waves' own
 // interleaving still overlaps the two).
-template <int NR, bool OPEN, bool ALIGNED, int G, int SPLIT, class RK, class GH>
+// WIN: keystream through the lane's 256-counter window cache at LDS ``win``
+// (aes_round.h, ctr_keystream).
+template <int NR, bool OPEN, bool ALIGNED, int G, int SPLIT, bool WIN, class RK, class GH>
 __device__ __forceinline__ uint4 ctr_groups(uint32_t lane4, const RK& rk, const GH& gh,
-                                            const CtrCache& cc, const uint8_t* in, uint8_t* out,
-                                            uint32_t ngroups, uint4 y) {
+                                            const CtrCache& cc, uint32_t win, const uint8_t* in,
+                                            uint8_t* out, uint32_t ngroups, uint4 y) {
     if (ngroups == 0) return y;
     uint4 d[G], ks[G];
 #pragma unroll
     for (int q = 0; q < G; ++q) d[q] = load16(in + 16 * q, ALIGNED);
-#pragma unroll
-    for (int q = 0; q < G; ++q) ks[q] = aes_ctr<NR>(lane4, rk, cc, 2u + q);
+    ctr_keystream<NR, G, WIN>(lane4, rk, cc, win, 2u, true, ks);
     for (uint32_t g = 0; g < ngroups; ++g) {
         const uint32_t gn = g + 1 < ngroups ? g + 1 : g;
         uint4 nx[G], c[G];
@@ -290,8 +291,7 @@ __device__ __forceinline__ uint4 ctr_groups(uint32_t lane4, const RK& rk, const 
             c[q] = xor4(d[q], ks[q]);
             store16(out + 16 * (G * g + q), c[q], ALIGNED);
         }
-#pragma unroll
-        for (int q = 0; q < G; ++q) ks[q] = aes_ctr<NR>(lane4, rk, cc, 2u + G * (g + 1) + q);
+        ctr_keystream<NR, G, WIN>(lane4, rk, cc, win, 2u + G * (g + 1), false, ks);
         if (SPLIT) __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
         for (int q = 0; q < G; ++q) y = gh.update(y, OPEN ? d[q] : c[q]);
@@ -302,9 +302,9 @@ __device__ __forceinline__ uint4 ctr_groups(uint32_t lane4, const RK& rk, const 
 }
 
 // One record: AESGCM.seal / AESGCM.open (aesgcm.py:101-154) for lane i.
-template <int NR, bool OPEN, int G, class RK, class GH, int SPLIT = 0>
+template <int NR, bool OPEN, int G, class RK, class GH, int SPLIT = 0, bool WIN = false>
 __device__ __forceinline__ void gcm_record(const tg_batch& b, uint64_t i, uint32_t lane4,
-                                           const RK& rk, const GH& gh) {
+                                           const RK& rk, const GH& gh, uint32_t win = 0) {
     const uint8_t* in = rec_in(b, i);
     uint8_t* out = rec_out(b, i);
     const uint32_t len = rec_len(b, i);
@@ -328,8 +328,9 @@ __device__ __forceinline__ void gcm_record(const tg_batch& b, uint64_t i, uint32
     const uint32_t nfull = len >> 4;
     const uint32_t tail = len & 15;
     const uint32_t ngroups = nfull / G;
-    y = aligned ? ctr_groups<NR, OPEN, true, G, SPLIT>(lane4, rk, gh, cc, in, out, ngroups, y)
-                : ctr_groups<NR, OPEN, false, G, SPLIT>(lane4, rk, gh, cc, in, out, ngroups, y);
+    y = aligned
+            ? ctr_groups<NR, OPEN, true, G, SPLIT, WIN>(lane4, rk, gh, cc, win, in, out, ngroups, y)
+            : ctr_groups<NR, OPEN, false, G, SPLIT, WIN>(lane4, rk, gh, cc, win, in, out, ngroups, y);
     for (uint32_t j = G * ngroups; j < nfull; ++j) {
         const uint4 ks = aes_ctr<NR>(lane4, rk, cc, 2u + j);
         const uint4 d = load16(in + 16 * j, aligned);
@@ -371,7 +372,8 @@ __device__ __forceinline__ void gcm_record(const tg_batch& b, uint64_t i, uint32
 template <int NR, bool OPEN, int G, int THREADS, int GH>
 __global__ __launch_bounds__(THREADS) void gcm_kernel(const GcmKeyDev* __restrict__ key,
                                                       tg_batch b, const uint32_t* __restrict__ order) {
-    constexpr int GHK = GH % 10, SPLIT = GH / 10;   // GHASH flavour, split schedule
+    constexpr int GHK = GH % 10, SPLIT = (GH / 10) % 10;   // GHASH flavour, split schedule
+    constexpr bool WIN = GH >= 100;                         // 256-counter window cache
     constexpr bool ROT = GHK != 0;
     uint4* lds = g_lds;
     // stage the GHASH tables (ROT: row layout b * 16 + j) and the Te0/Te2 copies
@@ -397,15 +399,17 @@ __global__ __launch_bounds__(THREADS) void gcm_kernel(const GcmKeyDev* __restric
     if (t >= b.n) return;
     const uint64_t i = order ? order[t] : t;
     const uint32_t lane4 = ((threadIdx.x & 31u) << 2) | kTeBase;
+    const uint32_t win = (uint32_t)kGcmLds + 16u * threadIdx.x;   // this lane's window slot
     if constexpr (GHK == 0) {
-        gcm_record<NR, OPEN, G, RkRegs<NR>, GhashTables, SPLIT>(b, i, lane4, rk, GhashTables{});
+        gcm_record<NR, OPEN, G, RkRegs<NR>, GhashTables, SPLIT, WIN>(b, i, lane4, rk,
+                                                                    GhashTables{}, win);
     } else if constexpr (GHK == 1) {
         GhashTablesRot gh;
         gh.init(threadIdx.x & 63);
-        gcm_record<NR, OPEN, G, RkRegs<NR>, GhashTablesRot, SPLIT>(b, i, lane4, rk, gh);
+        gcm_record<NR, OPEN, G, RkRegs<NR>, GhashTablesRot, SPLIT, WIN>(b, i, lane4, rk, gh, win);
     } else {
-        gcm_record<NR, OPEN, G, RkRegs<NR>, GhashTablesRotLds, SPLIT>(b, i, lane4, rk,
-                                                                     GhashTablesRotLds{lane4});
+        gcm_record<NR, OPEN, G, RkRegs<NR>, GhashTablesRotLds, SPLIT, WIN>(
+            b, i, lane4, rk, GhashTablesRotLds{lane4}, win);
     }
 }
 
@@ -1182,17 +1186,20 @@ int table_variant() {
 
 template <int NR, bool OPEN, int G, int THREADS, int GH>
 int launch_v(const GcmKeyDev* key, const tg_batch& b, hipStream_t s, const uint32_t* order) {
+    // GH >= 100: + one 16-byte window slot per thread after the fixed tables
+    constexpr size_t lds = kGcmLds + (GH >= 100 ? 16 * THREADS : 0);
+    static_assert(lds <= 160 * 1024, "LDS per workgroup");
     static bool attr_set = false;
     if (!attr_set) {
         if (hipFuncSetAttribute((const void*)gcm_kernel<NR, OPEN, G, THREADS, GH>,
-                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)kGcmLds) !=
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) !=
             hipSuccess)
             return TG_EHIP;
         attr_set = true;
     }
     const uint64_t blocks = (b.n + THREADS - 1) / THREADS;
     hipLaunchKernelGGL((gcm_kernel<NR, OPEN, G, THREADS, GH>), dim3((unsigned)blocks), dim3(THREADS),
-                       kGcmLds, s, key, b, order);
+                       lds, s, key, b, order);
     return hipGetLastError() == hipSuccess ? TG_OK : TG_EHIP;
 }
 
@@ -1222,11 +1229,13 @@ int launch(const GcmKeyDev* key, const tg_batch& b, hipStream_t s, const uint32_
         case 2: return launch_v<NR, OPEN, 2, 1024, 2>(key, b, s, order);
         case 3: return launch_v<NR, OPEN, 2, 512, 1>(key, b, s, order);
         case 4: return launch_bs<NR, OPEN>(key, b, s);
-        case 5: return launch_v<NR, OPEN, 4, 1024, 0>(key, b, s, order);
+        case 5: return launch_v<NR, OPEN, 4, 1024, 0>(key, b, s, order);   // no window cache
         case 6: return launch_wave<NR, OPEN>(key, b, s);
+        case 7: return launch_v<NR, OPEN, 4, 1024, 100>(key, b, s, order);
+        case 8: return launch_v<NR, OPEN, 2, 1024, 100>(key, b, s, order);
         default:
             if (b.n <= kWaveMaxRecords) return launch_wave<NR, OPEN>(key, b, s);
-            return launch_v<NR, OPEN, 4, 1024, 0>(key, b, s, order);
+            return launch_v<NR, OPEN, 4, 1024, 100>(key, b, s, order);
     }
 }
 

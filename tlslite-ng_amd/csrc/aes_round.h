@@ -183,6 +183,83 @@ __device__ __forceinline__ uint4 aes_ctr(uint32_t lane4, const RK& rkp, const Ct
     return aes_ctr_w<NR>(lane4, rkp, cc, bswap32(ctr));
 }
 
+// ---- 256-block counter windows (round-2 cache) ---------------------------
+// Within a window of 256 counters (ctr >> 8 fixed) only byte 15 of the
+// counter block changes.  After round 1 just state word 0 (A) depends on it
+// (the s3 byte-3 term of column 0); words 1..3 (B, C, D) are fixed, so each
+// round-2 column is a per-window constant W_c XOR the one lookup that reads
+// A.  A block then costs 1 + 4 lookups for rounds 1-2 instead of 4 + 16.
+// win_refresh computes W for the window holding ctr and stores it at the
+// lane's LDS slot ``win`` (16 B); aes_ctr_win runs one block from it.
+// Same function as aes_ctr (the windows are an algebraic regrouping of the
+// T-table rounds of rijndael.py:995-1038, not a different cipher).
+#if defined(__HIP_DEVICE_COMPILE__)
+__device__ __forceinline__ void lds_st_u128(uint32_t addr, uint4 v) {
+    *(__attribute__((address_space(3))) uint4*)(uintptr_t)addr = v;
+}
+#else
+__device__ __forceinline__ void lds_st_u128(uint32_t, uint4) {}
+#endif
+
+template <int NR, class RK>
+__device__ __forceinline__ void win_refresh(uint32_t lane4, const RK& rkp, const CtrCache& cc,
+                                            uint32_t win, uint32_t ctr) {
+    const uint32_t s3 = bswap32(ctr) ^ rkp.get(0).w;
+    const uint32_t B = cc.k1 ^ T2<2>(s3, lane4);
+    const uint32_t C = cc.k2 ^ rotl32(T0<1>(s3, lane4), 8);
+    const uint32_t D = cc.k3 ^ T0<0>(s3, lane4);
+    const uint4 k = rkp.get(2);
+    uint4 w;
+    w.x = xor3(T2<2>(C, lane4), k.x, rotl32(T0<1>(B, lane4) ^ T2<3>(D, lane4), 8));
+    w.y = xor3(T0<0>(B, lane4), T2<2>(D, lane4), k.y) ^ rotl32(T0<1>(C, lane4), 8);
+    w.z = xor3(T0<0>(C, lane4), k.z, rotl32(T0<1>(D, lane4) ^ T2<3>(B, lane4), 8));
+    w.w = xor3(T0<0>(D, lane4), T2<2>(B, lane4), k.w) ^ rotl32(T2<3>(C, lane4), 8);
+    lds_st_u128(win, w);
+}
+
+template <int NR, class RK>
+__device__ __forceinline__ uint4 aes_ctr_win(uint32_t lane4, const RK& rkp, const CtrCache& cc,
+                                             const uint4 w, uint32_t ctr) {
+    const uint32_t A = cc.k0 ^ rotl32(T2<3>((ctr << 24) ^ rkp.get(0).w, lane4), 8);
+    uint32_t s0 = w.x ^ T0<0>(A, lane4);
+    uint32_t s1 = w.y ^ rotl32(T2<3>(A, lane4), 8);
+    uint32_t s2 = w.z ^ T2<2>(A, lane4);
+    uint32_t s3 = w.w ^ rotl32(T0<1>(A, lane4), 8);
+    uint32_t t0, t1, t2, t3;
+#pragma unroll
+    for (int r = 3; r < NR; ++r) {
+        const uint4 k = rkp.get(r);
+        t0 = col(s0, s1, s2, s3, k.x, lane4);
+        t1 = col(s1, s2, s3, s0, k.y, lane4);
+        t2 = col(s2, s3, s0, s1, k.z, lane4);
+        t3 = col(s3, s0, s1, s2, k.w, lane4);
+        s0 = t0; s1 = t1; s2 = t2; s3 = t3;
+    }
+    const uint4 k = rkp.get(NR);
+    return make_uint4(col_last(s0, s1, s2, s3, k.x, lane4), col_last(s1, s2, s3, s0, k.y, lane4),
+                      col_last(s2, s3, s0, s1, k.z, lane4), col_last(s3, s0, s1, s2, k.w, lane4));
+}
+
+// Keystream of counters ctr0 .. ctr0 + G - 1.  WIN = 0: full rounds.  WIN:
+// through the window cache at LDS ``win``, refreshed when the group is the
+// first of a window (or ``first``); a group that straddles two windows runs
+// full rounds.  ctr0 is the same for every lane of a lane-per-record wave, so
+// both branches are wave-uniform.
+template <int NR, int G, bool WIN, class RK>
+__device__ __forceinline__ void ctr_keystream(uint32_t lane4, const RK& rkp, const CtrCache& cc,
+                                              uint32_t win, uint32_t ctr0, bool first,
+                                              uint4 (&ks)[G]) {
+    if (!WIN || ((ctr0 ^ (ctr0 + G - 1)) >> 8) != 0) {
+#pragma unroll
+        for (int q = 0; q < G; ++q) ks[q] = aes_ctr<NR>(lane4, rkp, cc, ctr0 + q);
+        return;
+    }
+    if (first || (ctr0 & 255u) < (uint32_t)G) win_refresh<NR>(lane4, rkp, cc, win, ctr0);
+    const uint4 w = lds_u128(win);
+#pragma unroll
+    for (int q = 0; q < G; ++q) ks[q] = aes_ctr_win<NR>(lane4, rkp, cc, w, ctr0 + q);
+}
+
 // Full AES encryption of one block (all rounds from the table).
 template <int NR, class RK>
 __device__ __forceinline__ uint4 aes_block(uint32_t lane4, const RK& rkp, uint4 in) {
