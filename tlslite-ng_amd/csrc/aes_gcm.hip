@@ -835,6 +835,10 @@ __device__ __forceinline__ void gcm_wave_record(const GcmKeyDev* __restrict__ ke
     const uint32_t wv = seg >> 6;              // the record's wave
     const uint64_t abits = (uint64_t)alen << 3, cbits = (uint64_t)len << 3;
     uint4 y = make_uint4(0, 0, 0, 0);
+    // 256-counter window cache in registers (aes_round.h): the lane's counter
+    // steps by 64, so it enters a new window every fourth block
+    uint4 wc = make_uint4(0, 0, 0, 0);
+    uint32_t whi = 0xffffffffu;
     for (uint32_t j = 0; j < Bw; ++j) {
         if (j) y = gmul(y);                     // y H^64 (wave-uniform)
         const uint32_t t = 64 * (Bw * wv + j) + lane;
@@ -846,7 +850,11 @@ __device__ __forceinline__ void gcm_wave_record(const GcmKeyDev* __restrict__ ke
             x = load_partial(ad + 16 * k, m);
         } else if (k < na + nc) {               // CTR block c (python_aes.py:101-116)
             const uint32_t c = k - na;
-            const uint4 ks = aes_ctr<NR>(lane4, rk, cc, 2u + c);
+            if (((2u + c) >> 8) != whi) {
+                whi = (2u + c) >> 8;
+                wc = win_consts<NR>(lane4, rk, cc, 2u + c);
+            }
+            const uint4 ks = aes_ctr_win<NR>(lane4, rk, cc, wc, 2u + c);
             if (c < nfull) {
                 const uint4 d = load16(in + 16 * c, aligned);
                 const uint4 ct = xor4(d, ks);
@@ -994,7 +1002,9 @@ __global__ __launch_bounds__(kMkThreads, 4) void gcm_table_kernel(const GcmTable
 // AES-256) instead of an LDS row: LDS holds only the 64 KiB Te block, so a
 // 768-thread workgroup (three waves per SIMD) fits where the LDS-row layout
 // (64 KiB + 68 KiB of rows) allowed one wave per SIMD.
-template <int NR, bool OPEN, int THREADS>
+// WIN: 256-counter window cache in a 16-byte LDS slot per lane after the Te
+// block (aes_round.h, ctr_keystream).
+template <int NR, bool OPEN, int THREADS, bool WIN = true>
 __global__ __launch_bounds__(THREADS) void gcm_table_vkernel(const GcmTableKey* __restrict__ keys,
                                                              tg_batch b,
                                                              const uint32_t* __restrict__ order) {
@@ -1009,21 +1019,23 @@ __global__ __launch_bounds__(THREADS) void gcm_table_vkernel(const GcmTableKey* 
     for (int k = 0; k < 4 * (NR + 1); ++k) rk.w[k] = kp->rk[k];
     const GhashClmul gh{*reinterpret_cast<const uint4*>(kp->hn)};
     const uint32_t lane4 = (threadIdx.x & 31u) << 2;
-    gcm_record<NR, OPEN, 1>(b, i, lane4, rk, gh);
+    gcm_record<NR, OPEN, 1, RkRegs<NR>, GhashClmul, 0, WIN>(b, i, lane4, rk, gh,
+                                                           65536u + 16u * threadIdx.x);
 }
 
-template <int NR, bool OPEN, int THREADS>
+template <int NR, bool OPEN, int THREADS, bool WIN = true>
 int launch_table_v(const GcmTableKey* keys, const tg_batch& b, hipStream_t s, const uint32_t* order) {
+    constexpr int lds = 65536 + (WIN ? 16 * THREADS : 0);
     static bool attr_set = false;
     if (!attr_set) {
-        if (hipFuncSetAttribute((const void*)gcm_table_vkernel<NR, OPEN, THREADS>,
-                                hipFuncAttributeMaxDynamicSharedMemorySize, 65536) != hipSuccess)
+        if (hipFuncSetAttribute((const void*)gcm_table_vkernel<NR, OPEN, THREADS, WIN>,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, lds) != hipSuccess)
             return TG_EHIP;
         attr_set = true;
     }
     const uint64_t blocks = (b.n + THREADS - 1) / THREADS;
-    hipLaunchKernelGGL((gcm_table_vkernel<NR, OPEN, THREADS>), dim3((unsigned)blocks), dim3(THREADS),
-                       65536, s, keys, b, order);
+    hipLaunchKernelGGL((gcm_table_vkernel<NR, OPEN, THREADS, WIN>), dim3((unsigned)blocks),
+                       dim3(THREADS), lds, s, keys, b, order);
     return hipGetLastError() == hipSuccess ? TG_OK : TG_EHIP;
 }
 
@@ -1061,6 +1073,8 @@ __device__ __forceinline__ void gcm_table_wave_record(const GcmTableKey* __restr
     const uint32_t Bw = (M + 63) >> 6, pad = 64 * Bw - M;
     const uint64_t abits = (uint64_t)alen << 3, cbits = (uint64_t)len << 3;
     uint4 y = make_uint4(0, 0, 0, 0);          // normal order
+    uint4 wc = make_uint4(0, 0, 0, 0);         // 256-counter window cache (aes_round.h)
+    uint32_t whi = 0xffffffffu;
     for (uint32_t j = 0; j < Bw; ++j) {
         if (j) y = gf128_mul(y, h64);           // y H^64 (wave-uniform)
         const uint32_t t = 64 * j + lane;
@@ -1072,7 +1086,11 @@ __device__ __forceinline__ void gcm_table_wave_record(const GcmTableKey* __restr
             x = load_partial(ad + 16 * k, m);
         } else if (k < na + nc) {               // CTR block c (python_aes.py:101-116)
             const uint32_t c = k - na;
-            const uint4 ks = aes_ctr<NR>(lane4, rk, cc, 2u + c);
+            if (((2u + c) >> 8) != whi) {
+                whi = (2u + c) >> 8;
+                wc = win_consts<NR>(lane4, rk, cc, 2u + c);
+            }
+            const uint4 ks = aes_ctr_win<NR>(lane4, rk, cc, wc, 2u + c);
             if (c < nfull) {
                 const uint4 d = load16(in + 16 * c, aligned);
                 const uint4 ct = xor4(d, ks);
@@ -1260,6 +1278,7 @@ int launch_table(const GcmTableKey* keys, const uint4* hpow, const tg_batch& b, 
     if (table_wave_path(b.n) && hpow) return launch_table_wave<NR, OPEN>(keys, hpow, b, s);
     switch (table_variant()) {
         case 2: return launch_table_v<NR, OPEN, 512>(keys, b, s, order);
+        case 6: return launch_table_v<NR, OPEN, 768, false>(keys, b, s, order);   // full rounds
         case 3: return launch_table_v<NR, OPEN, 1024>(keys, b, s, order);
         case 9: break;
         default: return launch_table_v<NR, OPEN, 768>(keys, b, s, order);

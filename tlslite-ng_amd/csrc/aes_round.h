@@ -202,8 +202,8 @@ __device__ __forceinline__ void lds_st_u128(uint32_t, uint4) {}
 #endif
 
 template <int NR, class RK>
-__device__ __forceinline__ void win_refresh(uint32_t lane4, const RK& rkp, const CtrCache& cc,
-                                            uint32_t win, uint32_t ctr) {
+__device__ __forceinline__ uint4 win_consts(uint32_t lane4, const RK& rkp, const CtrCache& cc,
+                                            uint32_t ctr) {
     const uint32_t s3 = bswap32(ctr) ^ rkp.get(0).w;
     const uint32_t B = cc.k1 ^ T2<2>(s3, lane4);
     const uint32_t C = cc.k2 ^ rotl32(T0<1>(s3, lane4), 8);
@@ -214,7 +214,13 @@ __device__ __forceinline__ void win_refresh(uint32_t lane4, const RK& rkp, const
     w.y = xor3(T0<0>(B, lane4), T2<2>(D, lane4), k.y) ^ rotl32(T0<1>(C, lane4), 8);
     w.z = xor3(T0<0>(C, lane4), k.z, rotl32(T0<1>(D, lane4) ^ T2<3>(B, lane4), 8));
     w.w = xor3(T0<0>(D, lane4), T2<2>(B, lane4), k.w) ^ rotl32(T2<3>(C, lane4), 8);
-    lds_st_u128(win, w);
+    return w;
+}
+
+template <int NR, class RK>
+__device__ __forceinline__ void win_refresh(uint32_t lane4, const RK& rkp, const CtrCache& cc,
+                                            uint32_t win, uint32_t ctr) {
+    lds_st_u128(win, win_consts<NR>(lane4, rkp, cc, ctr));
 }
 
 template <int NR, class RK>

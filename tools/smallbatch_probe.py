@@ -1,5 +1,5 @@
 """Device-resident throughput of small batches of 16 KiB records by kernel
-choice: record per lane (GCM variant 5 / ChaCha 4), one wave per record, four
+choice: record per lane (GCM variant 7 / ChaCha 4), one wave per record, four
 waves per record.  Sets the auto thresholds in aes_gcm.hip / chacha_poly.hip."""
 import os
 import sys
@@ -44,7 +44,7 @@ def run(obj, n, env):
 
 
 for name, obj, var, lane_v, wave_v in (
-        ("aes128gcm", tlsgpu.HipAESGCM(bytearray(16)), "TLSGPU_GCM_VARIANT", "5", "6"),
+        ("aes128gcm", tlsgpu.HipAESGCM(bytearray(16)), "TLSGPU_GCM_VARIANT", "7", "6"),
         ("chacha20-poly1305", tlsgpu.HipCHACHA20_POLY1305(bytearray(32)),
          "TLSGPU_CHACHA_VARIANT", "4", "3")):
     for n in (1, 4, 16, 64, 128, 256, 512, 1024, 2048, 4096, 16384, 65536):
@@ -59,10 +59,10 @@ for name, obj, var, lane_v, wave_v in (
 
 # where a record per lane overtakes a wave per record
 for name, obj, var, lane_v, wave_v in (
-        ("aes128gcm", tlsgpu.HipAESGCM(bytearray(16)), "TLSGPU_GCM_VARIANT", "5", "6"),
+        ("aes128gcm", tlsgpu.HipAESGCM(bytearray(16)), "TLSGPU_GCM_VARIANT", "7", "6"),
         ("chacha20-poly1305", tlsgpu.HipCHACHA20_POLY1305(bytearray(32)),
          "TLSGPU_CHACHA_VARIANT", "4", "3")):
-    for n in (32768, 131072, 262144, 524288, 1048576):
+    for n in (32768, 65536, 98304, 131072, 163840, 196608, 262144, 524288, 1048576):
         cols = []
         for label, env in (("lane", {var: lane_v}),
                            ("wave1", {var: wave_v, "TLSGPU_WAVES_PER_RECORD": "1"})):
