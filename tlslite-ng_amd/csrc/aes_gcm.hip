@@ -1231,9 +1231,10 @@ int launch_v(const GcmKeyDev* key, const tg_batch& b, hipStream_t s, const uint3
 // Up to this many records a batch runs one record per wavefront: a lane per
 // record leaves most of the GPU idle while one lane walks a whole record
 // until the batch fills every lane slot of the chip; at 16 KiB the two
-// kernels meet at 2^18 records (profiles/r01/v21_smallbatch.txt), and the
-// wave kernel needs no length planning for mixed batches.
-constexpr uint64_t kWaveMaxRecords = 262144;
+// kernels meet at 196 608 records since the lane kernel's counter-window
+// cache (profiles/r01/v31_smallbatch.txt; 2^18 before it, v21_smallbatch.txt),
+// and the wave kernel needs no length planning for mixed batches.
+constexpr uint64_t kWaveMaxRecords = 196608;
 
 int variant() {
     const char* e = getenv("TLSGPU_GCM_VARIANT");
