@@ -47,6 +47,8 @@ LENS = [0, 1, 15, 16, 17, 63, 64, 65, 1000, 1024, 1040, 4095, 16383, 16384, 1638
     ("aesgcm", 16, "TLSGPU_GCM_VARIANT", "7"),          # lane per record, counter windows
     ("aesgcm", 32, "TLSGPU_GCM_VARIANT", "7"),
     ("aesgcm", 16, "TLSGPU_GCM_VARIANT", "8"),          # windows, two blocks per group
+    ("aesgcm", 32, "TLSGPU_GCM_VARIANT", "9"),          # windows, rotated GHASH tables
+    ("aesgcm", 16, "TLSGPU_GCM_VARIANT", "13"),         # windows, three blocks per group
     ("aesgcm", 16, "TLSGPU_GCM_VARIANT", "6"),          # wave per record
     ("aesgcm", 32, "TLSGPU_GCM_VARIANT", "6"),
     ("chacha", 32, "TLSGPU_CHACHA_VARIANT", "4"),       # lane per record

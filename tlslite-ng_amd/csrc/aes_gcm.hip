@@ -1222,10 +1222,14 @@ int launch_v(const GcmKeyDev* key, const tg_batch& b, hipStream_t s, const uint3
 }
 
 // Kernel choice (TLSGPU_GCM_VARIANT, read per launch, for tests and measurement):
-//   0 / unset  T-table kernel, G = 4, 1024 threads, 8-bit GHASH tables (fastest
-//              measured: profiles/r01/gcm_variant_sweep.txt, bitsliced_gcm.txt);
+//   0 / unset  T-table kernel, G = 4, 1024 threads, counter-window cache, 8-bit
+//              GHASH tables (open) / rotated conflict-free tables (seal) (fastest
+//              measured: profiles/r01/gcm_variant_sweep.txt, bitsliced_gcm.txt,
+//              v33_gcm_window_sweep.txt);
 //   1..3       T-table tuning variants;
 //   4          the bitsliced kernel (gcm_bs_kernel);
+//   5          G = 4, 1024 threads, full rounds (no counter-window cache);
+//   7..13      counter-window tuning variants (G, threads, GHASH flavour);
 //   6          the wave-per-record kernel (gcm_wave_kernel), which is also what
 //              batches of at most kWaveMaxRecords records use.
 // Up to this many records a batch runs one record per wavefront: a lane per
@@ -1252,9 +1256,18 @@ int launch(const GcmKeyDev* key, const tg_batch& b, hipStream_t s, const uint32_
         case 6: return launch_wave<NR, OPEN>(key, b, s);
         case 7: return launch_v<NR, OPEN, 4, 1024, 100>(key, b, s, order);
         case 8: return launch_v<NR, OPEN, 2, 1024, 100>(key, b, s, order);
+        case 9: return launch_v<NR, OPEN, 4, 1024, 102>(key, b, s, order);
+        case 10: return launch_v<NR, OPEN, 2, 1024, 102>(key, b, s, order);
+        case 11: return launch_v<NR, OPEN, 2, 512, 101>(key, b, s, order);
+        case 12: return launch_v<NR, OPEN, 4, 768, 100>(key, b, s, order);
+        case 13: return launch_v<NR, OPEN, 3, 1024, 100>(key, b, s, order);
         default:
             if (b.n <= kWaveMaxRecords) return launch_wave<NR, OPEN>(key, b, s);
-            return launch_v<NR, OPEN, 4, 1024, 100>(key, b, s, order);
+            // seal hashes the ciphertext it has just produced: the conflict-free
+            // rotated GHASH (RL) is faster there, the plain tables for open
+            // (profiles/r01/v33_gcm_window_sweep.txt)
+            return OPEN ? launch_v<NR, OPEN, 4, 1024, 100>(key, b, s, order)
+                        : launch_v<NR, OPEN, 4, 1024, 102>(key, b, s, order);
     }
 }
 
