@@ -1,6 +1,8 @@
 """GPU parity of AES-CCM / CCM_8: libtlsgpu against the
 reference's fixtures (tests/golden/ccm.json, from make_golden_ccm.py) and the
 C oracle, bit-exact, through the C ABI."""
+import os
+
 import numpy as np
 import pytest
 
@@ -91,14 +93,24 @@ LEN_MIX = [0, 1, 15, 16, 17, 31, 63, 64, 65, 100, 255, 256, 1000, 1024, 1025, 40
 
 @pytest.mark.parametrize("klen,tl", [(16, 16), (32, 16), (16, 8), (32, 8)])
 @pytest.mark.parametrize("align", [16, 1])
-def test_batch_ragged_vs_oracle(torch, tg, oracle_mod, klen, tl, align):
+@pytest.mark.parametrize("variant", ["0", "1"])   # counter-window cache / full rounds
+def test_batch_ragged_vs_oracle(torch, tg, oracle_mod, klen, tl, align, variant):
     from batchpack import HostBatch, run_seal_open
     rng = np.random.default_rng(klen * 11 + tl + align)
-    lens = LEN_MIX * 4 + list(rng.integers(0, 16401, 150))
+    # + long records: many 256-counter windows
+    lens = LEN_MIX * 4 + list(rng.integers(0, 16401, 150)) + [65520, 65536, 70001]
     hb = HostBatch(lens, payload_seed=align + tl, align=align, aad_mode="random", tag=tl)
     key = rng.bytes(klen)
-    run_seal_open(torch, tg, oracle_mod, hb, "aesccm" if tl == 16 else "aesccm8",
-                  np.frombuffer(key, np.uint8), _obj(tg, key, tl), tamper=(3, 17, 100))
+    old = os.environ.get("TLSGPU_CCM_VARIANT")
+    os.environ["TLSGPU_CCM_VARIANT"] = variant
+    try:
+        run_seal_open(torch, tg, oracle_mod, hb, "aesccm" if tl == 16 else "aesccm8",
+                      np.frombuffer(key, np.uint8), _obj(tg, key, tl), tamper=(3, 17, 100))
+    finally:
+        if old is None:
+            del os.environ["TLSGPU_CCM_VARIANT"]
+        else:
+            os.environ["TLSGPU_CCM_VARIANT"] = old
 
 
 @pytest.mark.parametrize("klen,tl", [(16, 16), (32, 8)])

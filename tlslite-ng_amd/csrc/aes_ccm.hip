@@ -25,6 +25,8 @@
 // word nonce[11] | (bswap32(j) & 0xffffff00) for j < 2^24.  A record is
 // therefore limited to 2^24 - 2 blocks (256 MiB); past that the reference's
 // 128-bit increment would carry into the nonce (tlsgpu.h documents the limit).
+#include <stdlib.h>
+
 #include "aes_round.h"
 
 namespace tg {
@@ -45,7 +47,7 @@ __device__ __forceinline__ uint4 shl_bytes(uint4 v, uint32_t n) {
 
 __device__ __forceinline__ uint4 xor_blk(uint4 a, uint4 b) { return xor4(a, b); }
 
-template <int NR, bool OPEN, int TAG, class RK>
+template <int NR, bool OPEN, int TAG, bool WIN, class RK>
 __device__ __forceinline__ void ccm_record(const tg_batch& b, uint64_t i, uint32_t lane4,
                                            const RK& rk) {
     const uint8_t* in = rec_in(b, i);
@@ -89,13 +91,25 @@ __device__ __forceinline__ void ccm_record(const tg_batch& b, uint64_t i, uint32
     // payload: keystream S_1.., CBC-MAC over the plaintext (aesccm.py:68-70)
     const uint32_t nfull = len >> 4;
     const uint32_t tail = len & 15;
-    uint4 ks = aes_ctr_w<NR>(lane4, rk, cc, a3 | (bswap32(1u) & 0xffffff00u));
+    // keystream through the 256-counter window cache (aes_round.h): the
+    // counter is be24 in bytes 13..15, byte 15 its low byte as in GCM
+    uint4 wc = win_consts_w<NR>(lane4, rk, cc, a3);
+    uint32_t whi = 0;
+    uint4 ks = aes_ctr_win<NR>(lane4, rk, cc, wc, 1u);
     for (uint32_t j = 0; j < nfull; ++j) {
         const uint4 d = load16(in + 16 * j, aligned);
         const uint4 c = xor4(d, ks);
         store16(out + 16 * j, c, aligned);
         // next block's keystream is independent of this block's CBC step
-        ks = aes_ctr_w<NR>(lane4, rk, cc, a3 | (bswap32(j + 2u) & 0xffffff00u));
+        if (!WIN) {
+            ks = aes_ctr_w<NR>(lane4, rk, cc, a3 | (bswap32(j + 2u) & 0xffffff00u));
+        } else {
+            if (((j + 2u) >> 8) != whi) {      // all lanes at the same j: uniform
+                whi = (j + 2u) >> 8;
+                wc = win_consts_w<NR>(lane4, rk, cc, a3 | (bswap32(j + 2u) & 0xffffff00u));
+            }
+            ks = aes_ctr_win<NR>(lane4, rk, cc, wc, j + 2u);
+        }
         x = aes_block<NR>(lane4, rk, xor_blk(x, OPEN ? c : d));
     }
     if (tail) {
@@ -126,7 +140,9 @@ __device__ __forceinline__ void ccm_record(const tg_batch& b, uint64_t i, uint32
     }
 }
 
-template <int NR, bool OPEN, int TAG, bool TABLE>
+// WIN: the keystream through the 256-counter window cache (default);
+// TLSGPU_CCM_VARIANT=1 runs full rounds (measurement).
+template <int NR, bool OPEN, int TAG, bool TABLE, bool WIN>
 __global__ __launch_bounds__(ccm_threads<TABLE>()) void ccm_kernel(const AesKeyDev* __restrict__ keys,
                                                           tg_batch b) {
     stage_te(reinterpret_cast<uint32_t*>(g_lds_ccm));   // Te0/Te2 copies at LDS 0
@@ -138,14 +154,14 @@ __global__ __launch_bounds__(ccm_threads<TABLE>()) void ccm_kernel(const AesKeyD
 #pragma unroll
     for (int k = 0; k < 4 * (NR + 1); ++k) rk.w[k] = kp->rk[k];
     const uint32_t lane4 = (threadIdx.x & 31u) << 2;
-    ccm_record<NR, OPEN, TAG>(b, i, lane4, rk);
+    ccm_record<NR, OPEN, TAG, WIN>(b, i, lane4, rk);
 }
 
-template <int NR, bool OPEN, int TAG, bool TABLE>
-int launch(const AesKeyDev* keys, const tg_batch& b, hipStream_t s) {
+template <int NR, bool OPEN, int TAG, bool TABLE, bool WIN>
+int launch_w(const AesKeyDev* keys, const tg_batch& b, hipStream_t s) {
     static bool attr_set = false;
     if (!attr_set) {
-        if (hipFuncSetAttribute((const void*)ccm_kernel<NR, OPEN, TAG, TABLE>,
+        if (hipFuncSetAttribute((const void*)ccm_kernel<NR, OPEN, TAG, TABLE, WIN>,
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)kCcmLds) !=
             hipSuccess)
             return TG_EHIP;
@@ -153,9 +169,16 @@ int launch(const AesKeyDev* keys, const tg_batch& b, hipStream_t s) {
     }
     constexpr int threads = ccm_threads<TABLE>();
     const uint64_t blocks = (b.n + threads - 1) / threads;
-    hipLaunchKernelGGL((ccm_kernel<NR, OPEN, TAG, TABLE>), dim3((unsigned)blocks),
+    hipLaunchKernelGGL((ccm_kernel<NR, OPEN, TAG, TABLE, WIN>), dim3((unsigned)blocks),
                        dim3(threads), kCcmLds, s, keys, b);
     return hipGetLastError() == hipSuccess ? TG_OK : TG_EHIP;
+}
+
+template <int NR, bool OPEN, int TAG, bool TABLE>
+int launch(const AesKeyDev* keys, const tg_batch& b, hipStream_t s) {
+    const char* e = getenv("TLSGPU_CCM_VARIANT");   // read per launch (tests, measurement)
+    if (e && atoi(e) == 1) return launch_w<NR, OPEN, TAG, TABLE, false>(keys, b, s);
+    return launch_w<NR, OPEN, TAG, TABLE, true>(keys, b, s);
 }
 
 template <int NR, int TAG, bool TABLE>

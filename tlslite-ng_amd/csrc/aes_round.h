@@ -201,10 +201,12 @@ __device__ __forceinline__ void lds_st_u128(uint32_t addr, uint4 v) {
 __device__ __forceinline__ void lds_st_u128(uint32_t, uint4) {}
 #endif
 
+// w3: the counter block's last word as it sits in memory (its byte 3, the
+// counter's low byte, is ignored); win_consts(ctr) for the GCM layout.
 template <int NR, class RK>
-__device__ __forceinline__ uint4 win_consts(uint32_t lane4, const RK& rkp, const CtrCache& cc,
-                                            uint32_t ctr) {
-    const uint32_t s3 = bswap32(ctr) ^ rkp.get(0).w;
+__device__ __forceinline__ uint4 win_consts_w(uint32_t lane4, const RK& rkp, const CtrCache& cc,
+                                              uint32_t w3) {
+    const uint32_t s3 = w3 ^ rkp.get(0).w;
     const uint32_t B = cc.k1 ^ T2<2>(s3, lane4);
     const uint32_t C = cc.k2 ^ rotl32(T0<1>(s3, lane4), 8);
     const uint32_t D = cc.k3 ^ T0<0>(s3, lane4);
@@ -215,6 +217,12 @@ __device__ __forceinline__ uint4 win_consts(uint32_t lane4, const RK& rkp, const
     w.z = xor3(T0<0>(C, lane4), k.z, rotl32(T0<1>(D, lane4) ^ T2<3>(B, lane4), 8));
     w.w = xor3(T0<0>(D, lane4), T2<2>(B, lane4), k.w) ^ rotl32(T2<3>(C, lane4), 8);
     return w;
+}
+
+template <int NR, class RK>
+__device__ __forceinline__ uint4 win_consts(uint32_t lane4, const RK& rkp, const CtrCache& cc,
+                                            uint32_t ctr) {
+    return win_consts_w<NR>(lane4, rkp, cc, bswap32(ctr));
 }
 
 template <int NR, class RK>
