@@ -51,6 +51,8 @@ LENS = [0, 1, 15, 16, 17, 63, 64, 65, 1000, 1024, 1040, 4095, 16383, 16384, 1638
     ("aesgcm", 16, "TLSGPU_GCM_VARIANT", "13"),         # windows, three blocks per group
     ("aesgcm", 16, "TLSGPU_GCM_VARIANT", "6"),          # wave per record
     ("aesgcm", 32, "TLSGPU_GCM_VARIANT", "6"),
+    ("aesgcm", 16, "TLSGPU_GCM_VARIANT", "14"),         # 8-block bitsliced, octet per record
+    ("aesgcm", 32, "TLSGPU_GCM_VARIANT", "14"),
     ("chacha", 32, "TLSGPU_CHACHA_VARIANT", "4"),       # lane per record
     ("chacha", 32, "TLSGPU_CHACHA_VARIANT", "3"),       # wave per record
 ])
@@ -81,16 +83,17 @@ def test_auto_wave_per_record_batch(torch, tg, oracle_mod, alg, klen):
                   tamper=(0, 2047))
 
 
-@pytest.mark.parametrize("alg,klen,keys", [("aesgcm", 16, 1), ("chacha", 32, 1),
-                                          ("aesgcm", 32, 29), ("chacha", 32, 29)])
+@pytest.mark.parametrize("alg,klen,keys,gcmv", [("aesgcm", 16, 1, "7"), ("aesgcm", 16, 1, "14"),
+                                               ("chacha", 32, 1, None), ("aesgcm", 32, 29, None),
+                                               ("chacha", 32, 29, None)])
 @pytest.mark.parametrize("align", [16, 1])
-def test_planned_mixed_batch(torch, tg, oracle_mod, alg, klen, keys, align):
+def test_planned_mixed_batch(torch, tg, oracle_mod, alg, klen, keys, gcmv, align):
     """> 2048 records with per-record lengths on a lane-per-record kernel run
     longest first (planner.hip): every record must still land in its own
     output slot.  Single-key batches of this size run a wave per record by
     default, so the lane kernel is forced for them."""
     from batchpack import HostBatch, run_seal_open
-    rng = np.random.default_rng(1000 + klen + keys + align)
+    rng = np.random.default_rng(1000 + klen + keys + align + int(gcmv or 0))
     lens = list(rng.integers(0, 3000, 5000)) + [16384, 16400, 0, 1] * 5
     hb = HostBatch(lens, payload_seed=align, align=align, aad_mode="tls12", key_count=keys)
     kb = [rng.bytes(klen) for _ in range(keys)]
@@ -98,7 +101,7 @@ def test_planned_mixed_batch(torch, tg, oracle_mod, alg, klen, keys, align):
         obj = tg.HipAESGCM(bytearray(kb[0])) if alg == "aesgcm" else \
             tg.HipCHACHA20_POLY1305(bytearray(kb[0]))
         karr = np.frombuffer(kb[0], np.uint8)
-        env = ("TLSGPU_GCM_VARIANT", "7") if alg == "aesgcm" else ("TLSGPU_CHACHA_VARIANT", "4")
+        env = ("TLSGPU_GCM_VARIANT", gcmv) if alg == "aesgcm" else ("TLSGPU_CHACHA_VARIANT", "4")
     else:
         obj = tg.KeyTable("chacha20-poly1305" if alg == "chacha" else "aesgcm", kb)
         karr = np.frombuffer(b"".join(kb), np.uint8).reshape(keys, klen)

@@ -184,10 +184,14 @@ def test_config1_digest(torch, tg):
 
 # ------------------------------------------- full-size (BASELINE configs 2/3)
 
-@pytest.mark.parametrize("alg", ["aesgcm", "chacha"])
-def test_full_size_roundtrip_and_samples(torch, tg, oracle_mod, alg):
+@pytest.mark.parametrize("alg", ["aesgcm", "chacha", "aesgcm-bs8"])
+def test_full_size_roundtrip_and_samples(torch, tg, oracle_mod, alg, monkeypatch):
     """2^20 x 16 KiB records: seal -> open round trip on the whole batch
-    (size-independent property), and 64 sampled records bit-exact vs the oracle."""
+    (size-independent property), and 64 sampled records bit-exact vs the oracle.
+    aesgcm-bs8 forces the 8-block bitsliced kernel (TLSGPU_GCM_VARIANT=14)."""
+    if alg == "aesgcm-bs8":
+        monkeypatch.setenv("TLSGPU_GCM_VARIANT", "14")
+        alg = "aesgcm"
     n, L = 1 << 20, 16384
     g = torch.Generator(device="cuda").manual_seed(0x7715)
     inp = torch.randint(0, 256, (n * L,), dtype=torch.uint8, device="cuda", generator=g)

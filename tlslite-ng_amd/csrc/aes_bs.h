@@ -23,6 +23,9 @@
 // Usable from host code too (the CPU unit test compiles it with g++).
 #pragma once
 #include <stdint.h>
+#if defined(__HIPCC__)
+#include <hip/hip_runtime.h>
+#endif
 
 #if defined(__HIPCC__)
 #define TG_BS_HD __host__ __device__ __forceinline__

@@ -1,0 +1,222 @@
+// aes_bs8.h -- bitsliced AES counter mode for gfx950, 8 counter blocks per
+// lane in 32 registers ("row planes").
+//
+// Restates Rijndael.encrypt (tlslite/utils/rijndael.py:995-1038) on bit
+// planes, like aes_bs.h, but with a state small enough for four or more
+// waves per SIMD:
+//   * s[i][b] = bit plane b of state row i: byte c of the register is column
+//     c, bit j of that byte is block j of the lane's eight blocks;
+//   * SubBytes is the same 84-gate Boyar-Peralta circuit as aes_bs.h (one
+//     call covers the four bytes of a row for all eight blocks), its 0x63
+//     folded into the next round key;
+//   * ShiftRows rotates row i right by i bytes (one v_alignbit per plane);
+//   * MixColumns + AddRoundKey are plane XORs with the round-key planes as
+//     wave-uniform (scalar) operands;
+//   * the last round's ShiftRows is folded into the conversion back to block
+//     words (a byte gather by v_perm plus an 8 x 8 bit transpose per byte).
+// Counter blocks are nonce || be32(c), c = c0 + 64 beta + 8 j for block j of
+// batch beta (the GCM kernel gives a lane every eighth block of its record),
+// so bytes 0..11 are per-record constants, counter bits 0..5 per-lane
+// constants and only bits >= 6 change per batch (wave-uniformly).
+//
+// Usable from host code too (the CPU unit test compiles it with g++).
+#pragma once
+#include "aes_bs.h"
+
+namespace tg {
+namespace bs8 {
+
+#if !defined(__HIP_DEVICE_COMPILE__)
+using bs::bop3;   // a macro (one v_bitop3_b32) in device code
+#endif
+using bs::perm;
+using bs::xor3;
+
+// Rotate right by 8 i bits: byte c of the result = byte (c + i) % 4 of x.
+TG_BS_HD uint32_t rotr_bytes(uint32_t x, int i) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    return __builtin_amdgcn_alignbit(x, x, 8 * i);
+#else
+    return i ? (x >> (8 * i)) | (x << (32 - 8 * i)) : x;
+#endif
+}
+
+// Round-key plane (r, i, b) at index (4 r + i) 8 + b: byte c = 0xff iff bit b
+// of byte i of round-key word rk[4 r + c] ^ (r ? 0x63636363 : 0) is set
+// (the S-box constant dropped by the circuit, see aes_bs.h).  rk: LE words of
+// the schedule bytes (GcmKeyDev::rk).  (NR + 1) * 32 words per key.
+TG_BS_HD uint32_t mask_word(const uint32_t* rk, int e) {
+    const int r = e >> 5, i = (e >> 3) & 3, b = e & 7;
+    uint32_t m = 0;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+        const uint32_t w = rk[4 * r + c] ^ (r ? 0x63636363u : 0u);
+        if ((w >> (8 * i + b)) & 1u) m |= 0xffu << (8 * c);
+    }
+    return m;
+}
+
+struct KeyPlanes {   // key planes in memory (host: plain reads; device: scalar loads)
+    const uint32_t* w;
+    TG_BS_MF uint32_t operator()(int r, int i, int b) const {
+#if defined(__HIP_DEVICE_COMPILE__)
+        return ((const __attribute__((address_space(4))) uint32_t*)w)[(4 * r + i) * 8 + b];
+#else
+        return w[(4 * r + i) * 8 + b];
+#endif
+    }
+};
+
+// The per-record part of the first state (after AddRoundKey 0): plane e =
+// 8 i + b, byte c < 3 = bit e of u[c] (nonce word c ^ rk word c) spread to
+// 0x00 / 0xff, byte 3 = the same of rk word 3 (the counter column's key
+// byte; the counter itself is added per lane and batch).
+TG_BS_HD uint32_t rec_plane(const uint32_t u[4], int e) {
+    return (bs::bitmask(u[0], e) & 0x000000ffu) | (bs::bitmask(u[1], e) & 0x0000ff00u) |
+           (bs::bitmask(u[2], e) & 0x00ff0000u) | (bs::bitmask(u[3], e) & 0xff000000u);
+}
+
+// Per-lane counter constants for c0 = the lane's first counter (< 64):
+// counter bits 0..5 of block j are those of c0 + 8 j (no carry out of bit 5
+// except into the batch bits, see ctr_planes), as byte-3 planes lane[b] of
+// row 3; kmask = ~0 when c0 >= 8 (block 7 then carries into bit 6).
+TG_BS_HD void lane_consts(uint32_t c0, uint32_t lane[6], uint32_t& kmask) {
+#pragma unroll
+    for (int b = 0; b < 6; ++b) {
+        uint32_t m = 0;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) m |= (((c0 + 8u * j) >> b) & 1u) << j;
+        lane[b] = m << 24;
+    }
+    kmask = (c0 >> 3) & 1u ? 0xffffffffu : 0u;
+}
+
+// XOR the batch part of the counters (bits p >= 6: beta, or beta + 1 for
+// block 7 of lanes with kmask) into the state, for counter bits [P0, P1).
+// The kernel does bits 6..15 (rows 3 and 2) every batch and bits 16..31 only
+// once beta + 1 >= 2^10 (records over 1 MiB; a wave-uniform test).
+template <int P0, int P1>
+TG_BS_HD void ctr_planes(uint32_t (*s)[8], uint32_t kmask, uint32_t beta) {
+    const uint32_t flip = beta ^ (beta + 1u);
+#pragma unroll
+    for (int p = P0; p < P1; ++p) {
+        const uint32_t q = (uint32_t)(p - 6);
+        const uint32_t A = ((beta >> q) & 1u) ? 0xff000000u : 0u;
+        const uint32_t D = ((flip >> q) & 1u) ? 0x80000000u : 0u;
+        uint32_t& r = s[3 - (p >> 3)][p & 7];
+        r = bop3(r, kmask, D, 0x78) ^ A;   // r ^ (kmask & D) ^ A
+    }
+}
+
+// MixColumns(ShiftRows(x)) ^ K_r on the SubBytes output x, in place.
+// out_i = 2 (a_i ^ a_i+1) ^ a_i+1 ^ (a_i+2 ^ a_i+3) ^ k with a_i = row i of
+// the shifted state; 2x on planes: bit b <- bit b-1, bit 7 fed back into
+// bits 0, 1, 3, 4 (0x11b).  Plane by plane (t_i of plane 7 first, it feeds
+// the xtime of planes 0, 1, 3, 4), with scheduling fences between planes, so
+// that only about 48 state-sized values are live instead of a, t and the
+// output all at once (occupancy).
+#if defined(__HIP_DEVICE_COMPILE__)
+#define TG_BS8_FENCE() __builtin_amdgcn_sched_barrier(0)
+#else
+#define TG_BS8_FENCE() ((void)0)
+#endif
+template <class KM>
+TG_BS_HD void mix_round(uint32_t (*s)[8], const KM& km, int r) {
+    uint32_t a7[4], t7[4], tp[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) a7[i] = rotr_bytes(s[i][7], i);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) t7[i] = a7[i] ^ a7[(i + 1) & 3];
+    TG_BS8_FENCE();
+#pragma unroll
+    for (int b = 0; b < 8; ++b) {
+        uint32_t a[4], t[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) a[i] = b == 7 ? a7[i] : rotr_bytes(s[i][b], i);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) t[i] = b == 7 ? t7[i] : a[i] ^ a[(i + 1) & 3];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const uint32_t k = km(r, i, b);
+            const uint32_t tprev = b == 0 ? t7[i] : tp[i];
+            if (b == 1 || b == 3 || b == 4)
+                s[i][b] = xor3(xor3(tprev, t7[i], a[(i + 1) & 3]), t[(i + 2) & 3], k);
+            else
+                s[i][b] = xor3(tprev, a[(i + 1) & 3], t[(i + 2) & 3]) ^ k;
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) tp[i] = t[i];
+        TG_BS8_FENCE();
+    }
+}
+
+// 8 x 8 bit transpose inside every byte of a[0..7]: bit j of byte c of a[b]
+// <-> bit b of byte c of a[j] (three swap stages, two shifts + two bitop3
+// per pair).
+TG_BS_HD void transpose8(uint32_t* a) {
+#pragma unroll
+    for (int l = 2; l >= 0; --l) {
+        const int m = 1 << l;
+        const uint32_t mask = m == 4 ? 0x0f0f0f0fu : m == 2 ? 0x33333333u : 0x55555555u;
+#pragma unroll
+        for (int r = 0; r < 8; ++r) {
+            if (r & m) continue;
+            const uint32_t x = a[r], y = a[r + m];
+            a[r] = bop3(mask << m, y << m, x, 0xca);   // (y << m) where mask << m, else x
+            a[r + m] = bop3(mask, x >> m, y, 0xca);    // (x >> m) where mask, else y
+        }
+    }
+}
+
+// The last SubBytes output x (rows, pre-ShiftRows) -> block words:
+// w[q][j] = word q (column q, LE) of block j's keystream WITHOUT the last
+// round key.  Column q of the shifted state takes row i from column
+// (q + i) % 4, gathered by v_perm, then each column's eight planes are
+// transposed into the eight blocks.
+TG_BS_HD void to_blocks(uint32_t (*x)[8], uint32_t (*w)[8]) {
+#pragma unroll
+    for (int b = 0; b < 8; ++b) {
+        const uint32_t s0 = x[0][b], s1 = x[1][b], s2 = x[2][b], s3 = x[3][b];
+        const uint32_t A = perm(s1, s0, 0x07020500u);    // s0.0 s1.1 s0.2 s1.3
+        const uint32_t B = perm(s3, s2, 0x05000702u);    // s2.2 s3.3 s2.0 s3.1
+        const uint32_t A2 = perm(s1, s0, 0x04030601u);   // s0.1 s1.2 s0.3 s1.0
+        const uint32_t B2 = perm(s3, s2, 0x06010403u);   // s2.3 s3.0 s2.1 s3.2
+        w[0][b] = perm(B, A, 0x05040100u);
+        w[2][b] = perm(B, A, 0x07060302u);
+        w[1][b] = perm(B2, A2, 0x05040100u);
+        w[3][b] = perm(B2, A2, 0x07060302u);
+        TG_BS8_FENCE();
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        transpose8(w[q]);
+        TG_BS8_FENCE();
+    }
+}
+
+// Rounds 1..NR on the state after AddRoundKey 0 (in place); w receives the
+// blocks (to_blocks).  Middle rounds are a rolled loop on the device (a
+// round is ~500 instructions).
+template <int NR, class KM>
+TG_BS_HD void encrypt(uint32_t (*s)[8], const KM& km, uint32_t (*w)[8]) {
+#if defined(__HIP_DEVICE_COMPILE__)
+#pragma unroll 1
+#endif
+    for (int r = 1; r < NR; ++r) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            bs::sbox(s[i]);
+            TG_BS8_FENCE();
+        }
+        mix_round(s, km, r);
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        bs::sbox(s[i]);
+        TG_BS8_FENCE();
+    }
+    to_blocks(s, w);
+}
+
+}  // namespace bs8
+}  // namespace tg

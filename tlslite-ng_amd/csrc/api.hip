@@ -12,6 +12,7 @@
 #include <cstring>
 #include <string>
 
+#include "aes_bs8.h"
 #include "common.h"
 #include "tlsgpu.h"
 
@@ -592,6 +593,16 @@ int tg_key_create(int alg, const uint8_t* keys, size_t keylen, size_t nkeys, tg_
                     for (int q = 0; q < 4; ++q) h64[4 * w + q] = (uint8_t)(v >> (8 * q));
                 }
                 build_ghash_tables(h64, hk->ghash64);
+            }
+            {   // the tables of H^8 (gcm_bs8_kernel) and the bitsliced round-key planes
+                uint8_t h8[16];
+                const uint32_t pw[4] = {hk->hpow[7].x, hk->hpow[7].y, hk->hpow[7].z, hk->hpow[7].w};
+                for (int w = 0; w < 4; ++w) {
+                    const uint32_t v = tg::gcm_word_to_norm(pw[w]);
+                    for (int q = 0; q < 4; ++q) h8[4 * w + q] = (uint8_t)(v >> (8 * q));
+                }
+                build_ghash_tables(h8, hk->ghash8);
+                for (int e = 0; e < 32 * (nr + 1); ++e) hk->bs8mask[e] = tg::bs8::mask_word(hk->rk, e);
             }
             e = hipMalloc(&k->dev_key, sizeof(tg::GcmKeyDev));
             if (e == hipSuccess) e = hipMemcpy(k->dev_key, hk, sizeof(tg::GcmKeyDev), hipMemcpyHostToDevice);

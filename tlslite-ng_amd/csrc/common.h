@@ -27,6 +27,9 @@ struct GcmKeyDev {
     uint32_t bsmask[15 * 128];
     uint4 hpow[2048];      // H^1 .. H^kHPow, normal order (gcm_wave_kernel)
     uint4 ghash64[kGhashEntries];   // the 8-bit tables of H^64 (gcm_wave_kernel's stride)
+    uint4 ghash8[kGhashEntries];    // the 8-bit tables of H^8 (gcm_bs8_kernel's stride)
+    // 8-block bitsliced AES (aes_bs8.h): round-key plane (r, i, b) at (4 r + i) 8 + b
+    uint32_t bs8mask[15 * 32];
 };
 
 // Powers of H for the wave-per-record kernel: hpow[e - 1] = H^e in normal
@@ -197,6 +200,9 @@ inline int device_cus() {
 // t of a lane-per-record kernel handles record order[t].
 int tg_launch_gcm(const tg::GcmKeyDev* key, int rounds, const tg_batch& b, bool open,
                   hipStream_t s, const uint32_t* order = nullptr);
+// The 8-block bitsliced single-key kernel (aes_gcm_bs8.hip).
+int tg_launch_gcm_bs8(const tg::GcmKeyDev* key, int rounds, const tg_batch& b, bool open,
+                      hipStream_t s, const uint32_t* order);
 // hpow: the key table's GHASH powers (tg_launch_table_hpow), or NULL for the
 // lane-per-record kernels only.
 int tg_launch_gcm_table(const tg::GcmTableKey* keys, const uint4* hpow, int rounds,

@@ -1,0 +1,199 @@
+// ghash.h -- GHASH multiplies and single-block AES helpers shared by the
+// AES-GCM kernels (aes_gcm.hip, aes_gcm_bs8.hip) and the self-test entry
+// points (selftest.hip).
+//
+// GHASH (aesgcm.py:60-99, _mul :86-97, bit order :8-14) two ways:
+//   * gmul: y * G with the sixteen 8-bit tables of a fixed G staged in LDS
+//     at address 0 (entry (j, b) = b * x^(8j) * G at j * 4096 + b * 16);
+//   * gf128_mul: a table-free carry-less multiply of two arbitrary elements
+//     in normal polynomial order (key tables, the H-power lifts).
+// Included by exactly the kernel translation units; everything is internal.
+#pragma once
+#include "aes_round.h"
+
+namespace tg {
+namespace {
+
+// y * H with the sixteen 8-bit tables: X * H = XOR_j M_j[byte j of X]; byte j
+// of the block is byte j%4 of word j/4.  Entry (j, b) sits at j * 4096 + b * 16
+// (table j is the ds_read offset), so the 16 lanes of a ds_read_b128 group
+// land on the 16 bank slots by their own random bytes.
+__device__ __forceinline__ uint4 gmul(uint4 y) {
+    const uint32_t w[4] = {y.x, y.y, y.z, y.w};
+    uint4 e[16];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const uint32_t v = w[q];
+        e[4 * q + 0] = lds_u128(((v << 4) & 0xff0u) + 4096 * (4 * q + 0));
+        e[4 * q + 1] = lds_u128(((v >> 4) & 0xff0u) + 4096 * (4 * q + 1));
+        e[4 * q + 2] = lds_u128(((v >> 12) & 0xff0u) + 4096 * (4 * q + 2));
+        e[4 * q + 3] = lds_u128(((v >> 20) & 0xff0u) + 4096 * (4 * q + 3));
+    }
+    uint4 z = xor4_3(e[0], e[1], e[2]);
+    z = xor4_3(z, e[3], e[4]);
+    z = xor4_3(z, e[5], e[6]);
+    z = xor4_3(z, e[7], e[8]);
+    z = xor4_3(z, e[9], e[10]);
+    z = xor4_3(z, e[11], e[12]);
+    z = xor4_3(z, e[13], e[14]);
+    return xor4(z, e[15]);
+}
+
+// gmul with at most eight table rows in flight (32 VGPRs instead of 64), for
+// the bitsliced kernel whose keystream chunk already holds 128 VGPRs.
+__device__ __forceinline__ uint4 gmul_lowreg(uint4 y) {
+    const uint32_t w[4] = {y.x, y.y, y.z, y.w};
+    uint4 z = make_uint4(0, 0, 0, 0);
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        uint4 e[8];
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+            const uint32_t v = w[2 * h + q];
+            const int t = 4 * (2 * h + q);
+            e[4 * q + 0] = lds_u128(((v << 4) & 0xff0u) + 4096 * (t + 0));
+            e[4 * q + 1] = lds_u128(((v >> 4) & 0xff0u) + 4096 * (t + 1));
+            e[4 * q + 2] = lds_u128(((v >> 12) & 0xff0u) + 4096 * (t + 2));
+            e[4 * q + 3] = lds_u128(((v >> 20) & 0xff0u) + 4096 * (t + 3));
+        }
+        z = xor4_3(z, e[0], e[1]);
+        z = xor4_3(z, e[2], e[3]);
+        z = xor4_3(z, e[4], e[5]);
+        z = xor4_3(z, e[6], e[7]);
+        __builtin_amdgcn_sched_barrier(0);
+    }
+    return z;
+}
+
+// ---- table-free GHASH for key tables -----------------------------------
+// A key table cannot stage 64 KiB of GHASH tables per session, so each lane
+// multiplies by its own H with a carry-less multiply built from integer
+// multiplies (bits spaced four apart cannot carry into each other: a product
+// of two such words, masked to one residue class mod 4, is the carry-less
+// product on that class).  Elements are kept in normal polynomial order
+// (coefficient of x^i at bit i): a GCM block's bytes keep their positions and
+// each byte is bit-reversed (aesgcm.py:8-14).
+__device__ __forceinline__ uint32_t to_norm(uint32_t w) {
+    return bswap32(__builtin_bitreverse32(w));
+}
+
+__device__ __forceinline__ uint64_t mul32(uint32_t a, uint32_t b) { return (uint64_t)a * b; }
+
+__device__ __forceinline__ uint64_t clmul32(uint32_t x, uint32_t y) {
+    const uint32_t x0 = x & 0x11111111u, x1 = x & 0x22222222u, x2 = x & 0x44444444u,
+                   x3 = x & 0x88888888u;
+    const uint32_t y0 = y & 0x11111111u, y1 = y & 0x22222222u, y2 = y & 0x44444444u,
+                   y3 = y & 0x88888888u;
+    const uint64_t z0 = mul32(x0, y0) ^ mul32(x1, y3) ^ mul32(x2, y2) ^ mul32(x3, y1);
+    const uint64_t z1 = mul32(x0, y1) ^ mul32(x1, y0) ^ mul32(x2, y3) ^ mul32(x3, y2);
+    const uint64_t z2 = mul32(x0, y2) ^ mul32(x1, y1) ^ mul32(x2, y0) ^ mul32(x3, y3);
+    const uint64_t z3 = mul32(x0, y3) ^ mul32(x1, y2) ^ mul32(x2, y1) ^ mul32(x3, y0);
+    return (z0 & 0x1111111111111111ull) | (z1 & 0x2222222222222222ull) |
+           (z2 & 0x4444444444444444ull) | (z3 & 0x8888888888888888ull);
+}
+
+// 64 x 64 -> 128 by one Karatsuba step over 32-bit halves; result words w0..w3.
+// sched_barrier between the 32-bit products keeps the scheduler from running
+// all nine at once (each holds 16 64-bit partial products).
+__device__ __forceinline__ uint4 clmul64(uint32_t a0, uint32_t a1, uint32_t b0, uint32_t b1) {
+    const uint64_t lo = clmul32(a0, b0);
+    __builtin_amdgcn_sched_barrier(0);
+    const uint64_t hi = clmul32(a1, b1);
+    __builtin_amdgcn_sched_barrier(0);
+    const uint64_t mid = clmul32(a0 ^ a1, b0 ^ b1) ^ lo ^ hi;
+    __builtin_amdgcn_sched_barrier(0);
+    return make_uint4((uint32_t)lo, (uint32_t)(lo >> 32) ^ (uint32_t)mid,
+                      (uint32_t)(mid >> 32) ^ (uint32_t)hi, (uint32_t)(hi >> 32));
+}
+
+// a * b mod x^128 + x^7 + x^2 + x + 1, normal order, 32-bit limbs (x^0 in .x).
+__device__ __forceinline__ uint4 gf128_mul(uint4 a, uint4 b) {
+    const uint4 L = clmul64(a.x, a.y, b.x, b.y);
+    const uint4 Hh = clmul64(a.z, a.w, b.z, b.w);
+    const uint4 M = clmul64(a.x ^ a.z, a.y ^ a.w, b.x ^ b.z, b.y ^ b.w);
+    const uint32_t m0 = xor3(M.x, L.x, Hh.x), m1 = xor3(M.y, L.y, Hh.y);
+    const uint32_t m2 = xor3(M.z, L.z, Hh.z), m3 = xor3(M.w, L.w, Hh.w);
+    // 256-bit product p0..p7
+    const uint32_t p0 = L.x, p1 = L.y, p2 = L.z ^ m0, p3 = L.w ^ m1;
+    const uint32_t t0 = Hh.x ^ m2, t1 = Hh.y ^ m3, t2 = Hh.z, t3 = Hh.w;
+    // fold T = p4..p7 (x^128 == x^7 + x^2 + x + 1): r ^= T ^ T<<1 ^ T<<2 ^ T<<7
+    const uint32_t v = (t3 >> 31) ^ (t3 >> 30) ^ (t3 >> 25);  // bits pushed past x^127
+    uint32_t r0 = xor3(p0, t0, t0 << 1) ^ xor3(t0 << 2, t0 << 7, v);
+    r0 ^= xor3(v << 1, v << 2, v << 7);
+    const uint32_t r1 = xor3(p1, t1, t1 << 1) ^ xor3(t1 << 2, t1 << 7, (t0 >> 31)) ^
+                        ((t0 >> 30) ^ (t0 >> 25));
+    const uint32_t r2 = xor3(p2, t2, t2 << 1) ^ xor3(t2 << 2, t2 << 7, (t1 >> 31)) ^
+                        ((t1 >> 30) ^ (t1 >> 25));
+    const uint32_t r3 = xor3(p3, t3, t3 << 1) ^ xor3(t3 << 2, t3 << 7, (t2 >> 31)) ^
+                        ((t2 >> 30) ^ (t2 >> 25));
+    return make_uint4(r0, r1, r2, r3);
+}
+
+__device__ __forceinline__ uint4 shfl_xor4(uint4 v, int m) {
+    return make_uint4((uint32_t)__shfl_xor((int)v.x, m, 64), (uint32_t)__shfl_xor((int)v.y, m, 64),
+                      (uint32_t)__shfl_xor((int)v.z, m, 64), (uint32_t)__shfl_xor((int)v.w, m, 64));
+}
+
+__device__ __forceinline__ uint4 norm4(uint4 v) {
+    return make_uint4(to_norm(v.x), to_norm(v.y), to_norm(v.z), to_norm(v.w));
+}
+
+// x^e in GF(2^128), normal order (square and multiply): powers beyond the
+// key's table (records over ~18 KiB of AAD + payload).
+__device__ __forceinline__ uint4 gf128_pow(uint4 x, uint32_t e) {
+    uint4 r = make_uint4(1, 0, 0, 0);
+    while (e) {
+        if (e & 1) r = gf128_mul(r, x);
+        e >>= 1;
+        if (e) x = gf128_mul(x, x);
+    }
+    return r;
+}
+
+#if defined(__HIP_DEVICE_COMPILE__)
+__device__ __forceinline__ uint32_t lds_u8(uint32_t addr) {
+    return *(const __attribute__((address_space(3))) uint8_t*)(uintptr_t)addr;
+}
+#else
+__device__ __forceinline__ uint32_t lds_u8(uint32_t) { return 0; }
+#endif
+
+// S-box of each byte of w (256-byte LDS table at sbox)
+__device__ __forceinline__ uint32_t sub_word(uint32_t w, uint32_t sbox) {
+    return lds_u8(sbox + (w & 0xffu)) | (lds_u8(sbox + ((w >> 8) & 0xffu)) << 8) |
+           (lds_u8(sbox + ((w >> 16) & 0xffu)) << 16) | (lds_u8(sbox + (w >> 24)) << 24);
+}
+
+// MixColumns of one column packed as a LE word (byte i = row i):
+// out_i = 2 (a_i ^ a_i+1) ^ a_i+1 ^ a_i+2 ^ a_i+3.
+__device__ __forceinline__ uint32_t mix_word(uint32_t w) {
+    const uint32_t r1 = __builtin_amdgcn_alignbit(w, w, 8), r2 = __builtin_amdgcn_alignbit(w, w, 16),
+                   r3 = __builtin_amdgcn_alignbit(w, w, 24);
+    const uint32_t u = w ^ r1;
+    const uint32_t xt = ((u & 0x7f7f7f7fu) << 1) ^ (((u >> 7) & 0x01010101u) * 0x1bu);
+    return xt ^ xor3(r1, r2, r3);
+}
+
+// One block, byte-wise (rijndael.py:995-1038 restated): state words are the
+// columns, ShiftRows takes row i of column c from column (c + i) % 4.  For the
+// single blocks of the bitsliced kernels (tag masks, partial tails).
+template <int NR>
+__device__ __forceinline__ uint4 aes_block_sb(const uint32_t* rk, uint4 in, uint32_t sbox) {
+    uint32_t s[4] = {in.x ^ rk[0], in.y ^ rk[1], in.z ^ rk[2], in.w ^ rk[3]};
+#pragma unroll 1
+    for (int r = 1; r <= NR; ++r) {
+        uint32_t t[4];
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            const uint32_t w = __builtin_amdgcn_perm(s[(c + 1) & 3], s[c], 0x07060500u) & 0xffffu;
+            const uint32_t v = (s[(c + 2) & 3] & 0x00ff0000u) | (s[(c + 3) & 3] & 0xff000000u);
+            t[c] = sub_word(w | v, sbox);
+        }
+#pragma unroll
+        for (int c = 0; c < 4; ++c) s[c] = (r < NR ? mix_word(t[c]) : t[c]) ^ rk[4 * r + c];
+    }
+    return make_uint4(s[0], s[1], s[2], s[3]);
+}
+
+}  // namespace
+}  // namespace tg

@@ -16,6 +16,7 @@
 //                    layout (AesKeyDev).
 //   ghash_table_kernel  the 64 KiB single-key GHASH tables from H (the same
 //                    tables api.hip builds on the host).
+#include "aes_bs8.h"
 #include "common.h"
 
 namespace tg {
@@ -371,6 +372,16 @@ __global__ void ghash64_table_kernel(GcmKeyDev* key) {
     key->ghash64[e] = ghash_table_entry(hv, e);
 }
 
+// GcmKeyDev::ghash8: the same tables for H^8 (after hpow_kernel).
+__global__ void ghash8_table_kernel(GcmKeyDev* key) {
+    const int e = blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= kGhashEntries) return;
+    const uint4 p = key->hpow[7];
+    const uint32_t hv[4] = {gcm_word_to_norm(p.x), gcm_word_to_norm(p.y), gcm_word_to_norm(p.z),
+                            gcm_word_to_norm(p.w)};
+    key->ghash8[e] = ghash_table_entry(hv, e);
+}
+
 // GcmKeyDev::hpow: thread e computes H^(e+1) by square and multiply from H,
 // which aes_setup_kernel parked in ghash[0] (the table kernel leaves entry 0
 // alone and the launcher zeroes it after this kernel, stream-ordered).
@@ -392,6 +403,7 @@ __global__ void hpow_kernel(GcmKeyDev* key) {
 __global__ void bs_mask_kernel(GcmKeyDev* key) {
     const int e = blockIdx.x * blockDim.x + threadIdx.x;
     if (e < 128 * (int)(key->rounds + 1)) key->bsmask[e] = bs_mask_word(key->rk, e);
+    if (e < 32 * (int)(key->rounds + 1)) key->bs8mask[e] = bs8::mask_word(key->rk, e);
 }
 
 }  // namespace
@@ -437,6 +449,8 @@ int tg_launch_aes_setup(int keylen, int layout, const uint8_t* keys, uint64_t n,
         hipLaunchKernelGGL(tg::hpow_kernel, dim3((tg::kHPow + 255) / 256), dim3(256), 0, s, k);
         if (hipGetLastError() != hipSuccess) return TG_EHIP;
         hipLaunchKernelGGL(tg::ghash64_table_kernel, dim3(tg::kGhashEntries / 256), dim3(256), 0, s, k);
+        if (hipGetLastError() != hipSuccess) return TG_EHIP;
+        hipLaunchKernelGGL(tg::ghash8_table_kernel, dim3(tg::kGhashEntries / 256), dim3(256), 0, s, k);
         if (hipGetLastError() != hipSuccess) return TG_EHIP;
         hipLaunchKernelGGL(tg::bs_mask_kernel, dim3(15 * 128 / 256), dim3(256), 0, s, k);
         if (hipGetLastError() != hipSuccess) return TG_EHIP;
