@@ -53,6 +53,8 @@ LENS = [0, 1, 15, 16, 17, 63, 64, 65, 1000, 1024, 1040, 4095, 16383, 16384, 1638
     ("aesgcm", 32, "TLSGPU_GCM_VARIANT", "6"),
     ("aesgcm", 16, "TLSGPU_GCM_VARIANT", "14"),         # 8-block bitsliced, octet per record
     ("aesgcm", 32, "TLSGPU_GCM_VARIANT", "14"),
+    ("aesgcm", 16, "TLSGPU_GCM_VARIANT", "15"),         # hybrid T-table + bitsliced (persistent)
+    ("aesgcm", 32, "TLSGPU_GCM_VARIANT", "15"),
     ("chacha", 32, "TLSGPU_CHACHA_VARIANT", "4"),       # lane per record
     ("chacha", 32, "TLSGPU_CHACHA_VARIANT", "3"),       # wave per record
 ])

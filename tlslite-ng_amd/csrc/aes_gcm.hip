@@ -1043,16 +1043,18 @@ int launch_v(const GcmKeyDev* key, const tg_batch& b, hipStream_t s, const uint3
 }
 
 // Kernel choice (TLSGPU_GCM_VARIANT, read per launch, for tests and measurement):
-//   0 / unset  T-table kernel, G = 4, 1024 threads, counter-window cache, 8-bit
-//              GHASH tables (open) / rotated conflict-free tables (seal) (fastest
-//              measured: profiles/r01/gcm_variant_sweep.txt, bitsliced_gcm.txt,
-//              v33_gcm_window_sweep.txt);
+//   0 / unset  the wave-per-record kernel up to kWaveMaxRecords records, the
+//              hybrid octet kernel (15) above;
 //   1..3       T-table tuning variants;
 //   4          the bitsliced kernel (gcm_bs_kernel);
 //   5          G = 4, 1024 threads, full rounds (no counter-window cache);
 //   7..13      counter-window tuning variants (G, threads, GHASH flavour);
 //   6          the wave-per-record kernel (gcm_wave_kernel), which is also what
-//              batches of at most kWaveMaxRecords records use.
+//              batches of at most kWaveMaxRecords records use;
+//   14         the 8-block bitsliced octet kernel (aes_gcm_bs8.hip);
+//   15         the hybrid octet kernel (T-table + bitsliced waves), the default
+//              above kWaveMaxRecords (TLSGPU_HY_T / TLSGPU_HY_PRIO tune it);
+//   16         the T-table lane-per-record kernel that was the default before.
 // Up to this many records a batch runs one record per wavefront: a lane per
 // record leaves most of the GPU idle while one lane walks a whole record
 // until the batch fills every lane slot of the chip; at 16 KiB the two
@@ -1083,13 +1085,17 @@ int launch(const GcmKeyDev* key, const tg_batch& b, hipStream_t s, const uint32_
         case 12: return launch_v<NR, OPEN, 4, 768, 100>(key, b, s, order);
         case 13: return launch_v<NR, OPEN, 3, 1024, 100>(key, b, s, order);
         case 14: return tg_launch_gcm_bs8(key, NR, b, OPEN, s, order);
-        default:
-            if (b.n <= kWaveMaxRecords) return launch_wave<NR, OPEN>(key, b, s);
-            // seal hashes the ciphertext it has just produced: the conflict-free
-            // rotated GHASH (RL) is faster there, the plain tables for open
-            // (profiles/r01/v33_gcm_window_sweep.txt)
+        case 15: return tg_launch_gcm_hy(key, NR, b, OPEN, s, order);
+        case 16:
             return OPEN ? launch_v<NR, OPEN, 4, 1024, 100>(key, b, s, order)
                         : launch_v<NR, OPEN, 4, 1024, 102>(key, b, s, order);
+        default:
+            if (b.n <= kWaveMaxRecords) return launch_wave<NR, OPEN>(key, b, s);
+            // larger batches: the hybrid octet kernel (T-table waves beside
+            // bitsliced waves, aes_gcm_bs8.hip): 15.1 / 15.2 ms against the
+            // T-table lane kernel's 16.5 / 17.1 at 2^20 x 16 KiB
+            // (profiles/r02/v10_gcm_kernel_probe.txt)
+            return tg_launch_gcm_hy(key, NR, b, OPEN, s, order);
     }
 }
 

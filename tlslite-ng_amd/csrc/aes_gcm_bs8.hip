@@ -22,10 +22,11 @@
 //   * the nonce part of the first state is built once per record into LDS
 //     (32 planes, shared by the octet), the counter part per lane and batch
 //     from a few wave-uniform masks;
-//   * the tag mask E_K(J0) is one byte-wise AES block (S-box in LDS).
+//   * the tag mask E_K(J0) is one byte-wise AES block (S-box in LDS at ``sbox``).
 // LDS: the H^8 tables (64 KiB) + S-box + 4 KiB of record planes per 512-thread
 // workgroup, two workgroups per CU.
 #include <cstdlib>
+#include <type_traits>
 
 #include "aes_bs8.h"
 #include "aes_round.h"
@@ -36,9 +37,11 @@ namespace {
 
 constexpr int kBs8Threads = 512;
 constexpr int kBs8Recs = kBs8Threads / 8;               // record slots per workgroup
+constexpr uint32_t kTeBase = 65536;                       // hybrid kernel: Te0/Te2 copies
 constexpr uint32_t kBs8Sbox = 65536;                      // 256-byte S-box
-constexpr uint32_t kBs8RecBase = 65536 + 256;             // 128 B of planes per record slot
-constexpr size_t kBs8Lds = kBs8RecBase + kBs8Recs * 128;
+constexpr uint32_t kBs8Jt = 65536 + 256;                  // gmul_rot lane-offset rows (256 B)
+constexpr uint32_t kBs8RecBase = kBs8Jt + 256;            // 128 B of planes per record slot
+constexpr size_t kBs8Lds = kBs8RecBase + (kBs8Threads / 64) * 1024;
 
 // No static __shared__ in this file: the GHASH tables sit at LDS address 0
 // (gmul's absolute addresses).
@@ -62,21 +65,74 @@ __device__ __forceinline__ uint32_t wave_min_u32(uint32_t v) {
     return __builtin_amdgcn_readfirstlane(v);
 }
 
-template <int NR, bool OPEN>
-__global__ __launch_bounds__(kBs8Threads, 4) void gcm_bs8_kernel(const GcmKeyDev* __restrict__ key,
-                                                                tg_batch b,
-                                                                const uint32_t* __restrict__ order) {
-    for (int e = threadIdx.x; e < kGhashEntries; e += kBs8Threads) g_lds_bs8[e] = key->ghash8[e];
-    if (threadIdx.x < 64) {   // S(x) = byte 1 of Te0[x]
-        uint32_t v = 0;
+// The T-table keystream of half h of a lane's batch: counters c0 + 8 j,
+// j = 4 h .. 4 h + 3, in lock step (one round-key read per round for the four), through
+// the 256-counter window cache (aes_round.h) when no lane of the wave crosses
+// a window in this batch (a wave-uniform test), else full rounds.  Round keys
+// are read from LDS (wave-uniform address: one broadcast ds_read_b128 per
+// round), which keeps the 44 / 60 key words out of the SGPR file.
+template <int NR>
+__device__ __forceinline__ void t_half(uint32_t lane4, const RkLds& rk, const CtrCache& cc,
+                                       uint32_t c0, bool win, const uint4& wc, uint32_t k0w, int h,
+                                       uint4 (&ks)[4]) {
+    uint32_t s[4][4];
 #pragma unroll
-        for (int q = 0; q < 4; ++q) v |= ((c_te.te0[4 * threadIdx.x + q] >> 8) & 0xffu) << (8 * q);
-        reinterpret_cast<uint32_t*>(g_lds_bs8)[kBs8Sbox / 4 + threadIdx.x] = v;
+    for (int q = 0; q < 4; ++q) {
+        const uint32_t ctr = c0 + 8u * (4 * h + q);
+        if (win) {   // rounds 1-2 from the window constants (aes_ctr_win)
+            const uint32_t A = cc.k0 ^ rotl32(T2<3>((ctr << 24) ^ k0w, lane4), 8);
+            s[q][0] = wc.x ^ T0<0>(A, lane4);
+            s[q][1] = wc.y ^ rotl32(T2<3>(A, lane4), 8);
+            s[q][2] = wc.z ^ T2<2>(A, lane4);
+            s[q][3] = wc.w ^ rotl32(T0<1>(A, lane4), 8);
+        } else {     // round 1 from the record cache, then round 2 (aes_ctr_w)
+            const uint32_t s3 = bswap32(ctr) ^ k0w;
+            const uint32_t a0 = cc.k0 ^ rotl32(T2<3>(s3, lane4), 8);
+            const uint32_t a1 = cc.k1 ^ T2<2>(s3, lane4);
+            const uint32_t a2 = cc.k2 ^ rotl32(T0<1>(s3, lane4), 8);
+            const uint32_t a3 = cc.k3 ^ T0<0>(s3, lane4);
+            const uint4 k = rk.get(2);
+            s[q][0] = col(a0, a1, a2, a3, k.x, lane4);
+            s[q][1] = col(a1, a2, a3, a0, k.y, lane4);
+            s[q][2] = col(a2, a3, a0, a1, k.z, lane4);
+            s[q][3] = col(a3, a0, a1, a2, k.w, lane4);
+        }
     }
+#pragma unroll
+    for (int r = 3; r < NR; ++r) {
+        const uint4 k = rk.get(r);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const uint32_t t0 = col(s[q][0], s[q][1], s[q][2], s[q][3], k.x, lane4);
+            const uint32_t t1 = col(s[q][1], s[q][2], s[q][3], s[q][0], k.y, lane4);
+            const uint32_t t2 = col(s[q][2], s[q][3], s[q][0], s[q][1], k.z, lane4);
+            const uint32_t t3 = col(s[q][3], s[q][0], s[q][1], s[q][2], k.w, lane4);
+            s[q][0] = t0; s[q][1] = t1; s[q][2] = t2; s[q][3] = t3;
+        }
+    }
+    const uint4 k = rk.get(NR);
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+        ks[q] = make_uint4(col_last(s[q][0], s[q][1], s[q][2], s[q][3], k.x, lane4),
+                           col_last(s[q][1], s[q][2], s[q][3], s[q][0], k.y, lane4),
+                           col_last(s[q][2], s[q][3], s[q][0], s[q][1], k.z, lane4),
+                           col_last(s[q][3], s[q][0], s[q][1], s[q][2], k.w, lane4));
+}
+
+// One octet job: the eight records of record slots t0 .. t0 + 7 on this wave
+// (lane 8 q + l = lane l of slot t0 + q).  TROLE: the keystream comes from the
+// T-table cipher (aes_round.h, Te tables at kTeBase, round keys in SGPRs)
+// instead of the bitsliced one; everything else is shared.  ``recb``: this
+// wave's 1 KiB of LDS for the records' first-state planes.
+template <int NR, bool OPEN, bool TROLE>
+__device__ __forceinline__ void octet_job(const GcmKeyDev* __restrict__ key, const tg_batch& b,
+                                          const uint32_t* __restrict__ order, uint64_t t0,
+                                          uint32_t recw, const RkLds& rkT, uint32_t sbox,
+                                          uint32_t jt) {
     const uint32_t* rk = key->rk;
-    const uint32_t l = threadIdx.x & 7u;
-    const uint32_t slot = threadIdx.x >> 3;
-    const uint64_t t = (uint64_t)blockIdx.x * kBs8Recs + slot;
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t l = lane & 7u;
+    const uint64_t t = t0 + (lane >> 3);
     const bool valid = t < b.n;
     const uint64_t i = valid ? (order ? order[t] : t) : 0;
     uint32_t len = 0, alen = 0;
@@ -92,20 +148,20 @@ __global__ __launch_bounds__(kBs8Threads, 4) void gcm_bs8_kernel(const GcmKeyDev
         ad = rec_aad(b, i);
         nv = load_partial(b.nonce + 12 * i, 12);
     }
-    asm volatile("" ::: "memory");
     const uint32_t nfull = len >> 4, tail = len & 15, nc = (len + 15) >> 4, na = (alen + 15) >> 4;
     const uint32_t rho = (l + nc + 1u) & 7u;   // this lane's ciphertext blocks: rho + 8 v
-    const uint32_t recb = kBs8RecBase + slot * 128u;
-    {   // the record's first-state planes 4 l .. 4 l + 3 (nonce ^ rk0 spread to bytes)
+    const uint32_t recb = recw + (lane >> 3) * 128u;
+    const uint32_t lane4 = ((lane & 31u) << 2) | kTeBase;
+    CtrCache cc = {0, 0, 0, 0};
+    if (TROLE) {
+        cc = ctr_cache<NR>(lane4, rkT, nv);
+    } else {   // the record's first-state planes 4 l .. 4 l + 3 (nonce ^ rk0 spread to bytes)
         const uint32_t u[4] = {nv.x ^ rk[0], nv.y ^ rk[1], nv.z ^ rk[2], rk[3]};
         const uint4 rp = make_uint4(bs8::rec_plane(u, 4 * l), bs8::rec_plane(u, 4 * l + 1),
                                     bs8::rec_plane(u, 4 * l + 2), bs8::rec_plane(u, 4 * l + 3));
-        lds_st128(recb + 16u * l, rp);
+        lds_st128(recb + 16u * l, rp);   // read back by the same wave (LDS is in order per wave)
+        __builtin_amdgcn_wave_barrier();
     }
-    __syncthreads();
-
-    uint32_t lanec[6], kmask;
-    bs8::lane_consts(2u + rho, lanec, kmask);
     const bool aligned = (((uintptr_t)in | (uintptr_t)out) & 15) == 0;
     const uint32_t nvl = nc > rho ? (nc - rho + 7u) >> 3 : 0u;          // blocks of this lane
     const uint32_t nfl = nfull > rho ? (nfull - rho + 7u) >> 3 : 0u;    // full ones
@@ -117,55 +173,41 @@ __global__ __launch_bounds__(kBs8Threads, 4) void gcm_bs8_kernel(const GcmKeyDev
     uint4 y = make_uint4(0, 0, 0, 0);
     for (uint32_t a = (l + na + nc + 1u) & 7u; a < na; a += 8) {
         const uint32_t m = alen - 16 * a < 16 ? alen - 16 * a : 16;
-        y = xor4(gmul(y), load_partial(ad + 16 * a, m));
+        y = xor4(gmul_rot(y, lane & 15u, jt), load_partial(ad + 16 * a, m));
     }
 
     const bs8::KeyPlanes km{key->bs8mask};
-    const uint4 rkl = make_uint4(rk[4 * NR] ^ 0x63636363u, rk[4 * NR + 1] ^ 0x63636363u,
-                                 rk[4 * NR + 2] ^ 0x63636363u, rk[4 * NR + 3] ^ 0x63636363u);
-    for (uint32_t beta = 0; beta < nbatch; ++beta) {
-        uint32_t s[4][8];
-#pragma unroll
-        for (int q = 0; q < 8; ++q) {
-            const uint4 v = lds_u128(recb + 16u * q);
-            s[q >> 1][4 * (q & 1) + 0] = v.x;
-            s[q >> 1][4 * (q & 1) + 1] = v.y;
-            s[q >> 1][4 * (q & 1) + 2] = v.z;
-            s[q >> 1][4 * (q & 1) + 3] = v.w;
-        }
-#pragma unroll
-        for (int bb = 0; bb < 6; ++bb) s[3][bb] ^= lanec[bb];
-        bs8::ctr_planes<6, 16>(s, kmask, beta);
-        if ((beta + 1u) >> 10) bs8::ctr_planes<16, 32>(s, kmask, beta);
-        uint32_t w[4][8];
-        bs8::encrypt<NR>(s, km, w);
-        const uint32_t blk0 = rho + 64u * beta;   // block of slot j: blk0 + 8 j
-        auto ks = [&](int j) { return make_uint4(w[0][j], w[1][j], w[2][j], w[3][j]); };
-        if (beta < nfast) {
+    // the bitsliced cipher leaves out the last round key (folded into the XOR)
+    const uint4 rkl = TROLE ? make_uint4(0, 0, 0, 0)
+                            : make_uint4(rk[4 * NR] ^ 0x63636363u, rk[4 * NR + 1] ^ 0x63636363u,
+                                         rk[4 * NR + 2] ^ 0x63636363u, rk[4 * NR + 3] ^ 0x63636363u);
+    // XOR + store of N consecutive slots j0 .. j0 + N - 1 (the keystream dies
+    // block by block), then the GHASH chain over their inputs
+    auto consume = [&](const uint4* ks, uint32_t blk0, int j0, auto NN) {
+        constexpr int N = decltype(NN)::value;
+        if (blk0 < (nfast << 6)) {   // every valid lane of the wave has these blocks full
             if (valid) {
-                // XOR + store first (the keystream dies block by block), then the
-                // GHASH chain over the eight inputs held in d
-                uint4 d[8];
+                uint4 d[N];
 #pragma unroll
-                for (int j = 0; j < 8; ++j)
-                    d[j] = *reinterpret_cast<const uint4*>(in + 16u * (blk0 + 8u * j));
+                for (int q = 0; q < N; ++q)
+                    d[q] = *reinterpret_cast<const uint4*>(in + 16u * (blk0 + 8u * (j0 + q)));
 #pragma unroll
-                for (int j = 0; j < 8; ++j) {
-                    const uint4 k = ks(j);
-                    const uint4 c = make_uint4(xor3(d[j].x, k.x, rkl.x), xor3(d[j].y, k.y, rkl.y),
-                                               xor3(d[j].z, k.z, rkl.z), xor3(d[j].w, k.w, rkl.w));
-                    *reinterpret_cast<uint4*>(out + 16u * (blk0 + 8u * j)) = c;
-                    if (!OPEN) d[j] = c;
+                for (int q = 0; q < N; ++q) {
+                    const uint4 k = ks[q];
+                    const uint4 c = make_uint4(xor3(d[q].x, k.x, rkl.x), xor3(d[q].y, k.y, rkl.y),
+                                               xor3(d[q].z, k.z, rkl.z), xor3(d[q].w, k.w, rkl.w));
+                    *reinterpret_cast<uint4*>(out + 16u * (blk0 + 8u * (j0 + q))) = c;
+                    if (!OPEN) d[q] = c;
                 }
 #pragma unroll
-                for (int j = 0; j < 8; ++j) y = xor4(gmul_lowreg(y), d[j]);
+                for (int q = 0; q < N; ++q) y = xor4(gmul_rot(y, lane & 15u, jt), d[q]);
             }
         } else {
 #pragma unroll
-            for (int j = 0; j < 8; ++j) {
-                const uint32_t blk = blk0 + 8u * j;
+            for (int q = 0; q < N; ++q) {
+                const uint32_t blk = blk0 + 8u * (j0 + q);
                 if (!valid || blk >= nc) continue;
-                const uint4 k = ks(j);
+                const uint4 k = ks[q];
                 const uint4 kk = make_uint4(k.x ^ rkl.x, k.y ^ rkl.y, k.z ^ rkl.z, k.w ^ rkl.w);
                 uint4 d, c;
                 if (blk < nfull) {
@@ -177,15 +219,55 @@ __global__ __launch_bounds__(kBs8Threads, 4) void gcm_bs8_kernel(const GcmKeyDev
                     c = mask_tail(xor4(d, kk), tail);
                     store_partial(out + 16u * blk, c, tail);
                 }
-                y = xor4(gmul_lowreg(y), OPEN ? d : c);
+                y = xor4(gmul_rot(y, lane & 15u, jt), OPEN ? d : c);
             }
+        }
+    };
+    for (uint32_t beta = 0; beta < nbatch; ++beta) {
+        const uint32_t blk0 = rho + 64u * beta;   // block of slot j: blk0 + 8 j
+        const uint32_t c0 = 2u + blk0;             // its counter: c0 + 8 j
+        if (TROLE) {
+            // through the 256-counter window cache when no lane of the wave
+            // crosses a window in this batch (wave-uniform); two halves of four
+            const bool win = __all(((c0 ^ (c0 + 56u)) >> 8) == 0);
+            const uint32_t k0w = rkT.get(0).w;
+            const uint4 wc = win ? win_consts<NR>(lane4, rkT, cc, c0) : make_uint4(0, 0, 0, 0);
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                uint4 ks[4];
+                t_half<NR>(lane4, rkT, cc, c0, win, wc, k0w, h, ks);
+                consume(ks, blk0, 4 * h, std::integral_constant<int, 4>());
+                __builtin_amdgcn_sched_barrier(0);
+            }
+        } else {
+            uint32_t s[4][8];
+#pragma unroll
+            for (int q = 0; q < 8; ++q) {
+                const uint4 v = lds_u128(recb + 16u * q);
+                s[q >> 1][4 * (q & 1) + 0] = v.x;
+                s[q >> 1][4 * (q & 1) + 1] = v.y;
+                s[q >> 1][4 * (q & 1) + 2] = v.z;
+                s[q >> 1][4 * (q & 1) + 3] = v.w;
+            }
+            uint32_t lanec[6], kmask;
+            bs8::lane_consts(c0, lanec, kmask);
+#pragma unroll
+            for (int bb = 0; bb < 6; ++bb) s[3][bb] ^= lanec[bb];
+            bs8::ctr_planes<6, 16>(s, kmask, beta);
+            if ((beta + 1u) >> 10) bs8::ctr_planes<16, 32>(s, kmask, beta);
+            uint32_t w[4][8];
+            bs8::encrypt<NR>(s, km, w);
+            uint4 ks[8];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) ks[j] = make_uint4(w[0][j], w[1][j], w[2][j], w[3][j]);
+            consume(ks, blk0, 0, std::integral_constant<int, 8>());
         }
     }
     if (!__any(valid)) return;
     // length block be64(8 alen) || be64(8 len) (aesgcm.py:64): the last position
     if (l == 7) {
         const uint64_t abits = (uint64_t)alen << 3, cbits = (uint64_t)len << 3;
-        y = xor4(gmul(y), make_uint4(bswap32((uint32_t)(abits >> 32)), bswap32((uint32_t)abits),
+        y = xor4(gmul_rot(y, lane & 15u, jt), make_uint4(bswap32((uint32_t)(abits >> 32)), bswap32((uint32_t)abits),
                                      bswap32((uint32_t)(cbits >> 32)), bswap32((uint32_t)cbits)));
     }
     // lift by H^(8 - l) and XOR-reduce over the octet
@@ -195,7 +277,8 @@ __global__ __launch_bounds__(kBs8Threads, 4) void gcm_bs8_kernel(const GcmKeyDev
     for (int m = 1; m < 8; m <<= 1) yn = xor4(yn, shfl_xor4(yn, m));
     // tag = GHASH ^ E_K(J0), J0 = nonce || be32(1) (aesgcm.py:112-122)
     if (valid) nv = load_partial(b.nonce + 12 * i, 12);   // reloaded: not held across the loop
-    const uint4 mask = aes_block_sb<NR>(rk, make_uint4(nv.x, nv.y, nv.z, bswap32(1u)), kBs8Sbox);
+    const uint4 mask = TROLE ? aes_ctr<NR>(lane4, rkT, cc, 1u)
+                             : aes_block_sb<NR>(rk, make_uint4(nv.x, nv.y, nv.z, bswap32(1u)), sbox);
     const uint4 tag = xor4(norm4(yn), mask);
     const bool tag_aligned = aligned && tail == 0;
     if (!OPEN) {
@@ -209,12 +292,99 @@ __global__ __launch_bounds__(kBs8Threads, 4) void gcm_bs8_kernel(const GcmKeyDev
         diff = (exp.x ^ tag.x) | (exp.y ^ tag.y) | (exp.z ^ tag.z) | (exp.w ^ tag.w);
         if (b.status) b.status[i] = diff == 0;
     }
-    diff = (uint32_t)__shfl((int)diff, (int)(threadIdx.x & 56u), 64);
+    diff = (uint32_t)__shfl((int)diff, (int)(lane & 56u), 64);
     if (valid && diff) {   // a rejected record's plaintext is zeroed: each lane its own blocks
         const uint4 z = make_uint4(0, 0, 0, 0);
         for (uint32_t blk = rho; blk < nfull; blk += 8) store16(out + 16u * blk, z, aligned);
         if (tail && (nfull & 7u) == rho) store_partial(out + 16u * nfull, z, tail);
     }
+}
+
+__device__ __forceinline__ void stage_sbox(uint32_t base) {
+    if (threadIdx.x < 64) {   // S(x) = byte 1 of Te0[x]
+        uint32_t v = 0;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) v |= ((c_te.te0[4 * threadIdx.x + q] >> 8) & 0xffu) << (8 * q);
+        reinterpret_cast<uint32_t*>(g_lds_bs8)[base / 4 + threadIdx.x] = v;
+    }
+}
+
+// All-bitsliced grid: one job per wave, kBs8Recs records per workgroup.
+template <int NR, bool OPEN>
+__global__ __launch_bounds__(kBs8Threads, 4) void gcm_bs8_kernel(const GcmKeyDev* __restrict__ key,
+                                                                tg_batch b,
+                                                                const uint32_t* __restrict__ order) {
+    stage_ghash_rot(g_lds_bs8, key->ghash8, kBs8Jt);
+    stage_sbox(kBs8Sbox);
+    __syncthreads();
+    const uint32_t wave = threadIdx.x >> 6;
+    octet_job<NR, OPEN, false>(key, b, order, (uint64_t)blockIdx.x * kBs8Recs + 8u * wave,
+                               kBs8RecBase + wave * 1024u, RkLds{0}, kBs8Sbox, kBs8Jt);
+}
+
+// ---- hybrid persistent kernel: T-table waves beside bitsliced waves -------
+// The T-table cipher is bound by LDS lookups with the VALU ~35 % busy, the
+// bitsliced one by the VALU; one workgroup per CU runs both kinds of wave
+// (waves 0 .. nt-1 T-table at raised priority, the rest bitsliced), each
+// taking octet jobs (8 records) from a global queue until the batch is done,
+// so the LDS and the VALU are busy at the same time.
+// LDS: H^8 tables [0, 64K), Te0/Te2 copies [64K, 128K), S-box, then 1 KiB of
+// record planes per wave.
+constexpr int kHyThreads = 1024;
+constexpr uint32_t kHySbox = 2 * 65536;
+constexpr uint32_t kHyRk = kHySbox + 256;               // 15 round keys (16 B each)
+constexpr uint32_t kHyJt = kHyRk + 256;                 // gmul_rot lane-offset rows
+constexpr uint32_t kHyRecBase = kHyJt + 256;
+constexpr size_t kHyLds = kHyRecBase + (kHyThreads / 64) * 1024;
+static_assert(kTeBase == 65536, "Te block follows the GHASH tables");
+
+// The batch descriptor is read from memory per job (bp): held in SGPRs
+// across the persistent loop it would crowd out the ciphers' own scalars.
+template <int NR, bool OPEN>
+__global__ __launch_bounds__(kHyThreads) void gcm_hy_kernel(const GcmKeyDev* __restrict__ key,
+                                                            const tg_batch* bp,
+                                                            const uint32_t* __restrict__ order,
+                                                            uint32_t* __restrict__ queue,
+                                                            uint32_t nt, uint32_t prio) {
+    stage_ghash_rot(g_lds_bs8, key->ghash8, kHyJt);
+    stage_te(reinterpret_cast<uint32_t*>(g_lds_bs8) + kTeBase / 4);
+    stage_sbox(kHySbox);
+    if (threadIdx.x < 4 * (NR + 1)) reinterpret_cast<uint32_t*>(g_lds_bs8)[kHyRk / 4 + threadIdx.x] = key->rk[threadIdx.x];
+    __syncthreads();
+    const uint32_t wave = (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    const uint64_t njobs = (bp->n + 7) / 8;
+    const uint32_t recw = kHyRecBase + wave * 1024u;
+    if (wave < nt) {
+        if (prio) __builtin_amdgcn_s_setprio(1);
+        const RkLds rk{kHyRk};
+        for (;;) {
+            uint32_t job = 0;
+            if ((threadIdx.x & 63u) == 0) job = atomicAdd(queue, 1u);
+            job = (uint32_t)__builtin_amdgcn_readfirstlane((int)job);
+            if (job >= njobs) break;
+            asm volatile("" ::: "memory");
+            const tg_batch b = *bp;
+            octet_job<NR, OPEN, true>(key, b, order, 8ull * job, recw, rk, kHySbox, kHyJt);
+        }
+    } else {
+        const RkLds none{0};
+        for (;;) {
+            uint32_t job = 0;
+            if ((threadIdx.x & 63u) == 0) job = atomicAdd(queue, 1u);
+            job = (uint32_t)__builtin_amdgcn_readfirstlane((int)job);
+            if (job >= njobs) break;
+            asm volatile("" ::: "memory");
+            const tg_batch b = *bp;
+            octet_job<NR, OPEN, false>(key, b, order, 8ull * job, recw, none, kHySbox, kHyJt);
+        }
+    }
+}
+
+// Stream-ordered setup of the hybrid kernel's scratch: the job counter and a
+// device copy of the batch descriptor.
+__global__ void hy_setup_kernel(tg_batch b, uint32_t* queue, tg_batch* bcopy) {
+    *queue = 0;
+    *bcopy = b;
 }
 
 template <int NR, bool OPEN>
@@ -233,8 +403,50 @@ int launch_bs8(const GcmKeyDev* key, const tg_batch& b, hipStream_t s, const uin
     return hipGetLastError() == hipSuccess ? TG_OK : TG_EHIP;
 }
 
+// TLSGPU_HY_T (T-table waves per 16, default 8) and TLSGPU_HY_PRIO (default 1)
+// are read per launch (measurement).
+template <int NR, bool OPEN>
+int launch_hy(const GcmKeyDev* key, const tg_batch& b, hipStream_t s, const uint32_t* order) {
+    static bool attr_set = false;
+    if (!attr_set) {
+        if (hipFuncSetAttribute((const void*)gcm_hy_kernel<NR, OPEN>,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)kHyLds) != hipSuccess)
+            return TG_EHIP;
+        attr_set = true;
+    }
+    if ((b.n + 7) / 8 > 0xffffffffull) return TG_EINVAL;
+    const char* et = getenv("TLSGPU_HY_T");
+    const char* ep = getenv("TLSGPU_HY_PRIO");
+    const uint32_t nt = et ? (uint32_t)atoi(et) : 8u;
+    const uint32_t prio = ep ? (uint32_t)atoi(ep) : 1u;
+    // job counter + batch copy: stream-ordered scratch, so concurrent batches
+    // never share them
+    uint8_t* scratch = nullptr;
+    if (hipMallocAsync((void**)&scratch, 256, s) != hipSuccess) return TG_EHIP;
+    uint32_t* queue = reinterpret_cast<uint32_t*>(scratch);
+    tg_batch* bcopy = reinterpret_cast<tg_batch*>(scratch + 64);
+    hipLaunchKernelGGL(hy_setup_kernel, dim3(1), dim3(1), 0, s, b, queue, bcopy);
+    bool ok = hipGetLastError() == hipSuccess;
+    if (ok) {
+        hipLaunchKernelGGL((gcm_hy_kernel<NR, OPEN>), dim3((unsigned)device_cus()), dim3(kHyThreads), kHyLds,
+                           s, key, (const tg_batch*)bcopy, order, queue, nt, prio);
+        ok = hipGetLastError() == hipSuccess;
+    }
+    if (hipFreeAsync(scratch, s) != hipSuccess) return TG_EHIP;
+    return ok ? TG_OK : TG_EHIP;
+}
+
 }  // namespace
 }  // namespace tg
+
+int tg_launch_gcm_hy(const tg::GcmKeyDev* key, int rounds, const tg_batch& b, bool open,
+                     hipStream_t s, const uint32_t* order) {
+    if (rounds == 10)
+        return open ? tg::launch_hy<10, true>(key, b, s, order) : tg::launch_hy<10, false>(key, b, s, order);
+    if (rounds == 14)
+        return open ? tg::launch_hy<14, true>(key, b, s, order) : tg::launch_hy<14, false>(key, b, s, order);
+    return TG_EINVAL;
+}
 
 int tg_launch_gcm_bs8(const tg::GcmKeyDev* key, int rounds, const tg_batch& b, bool open,
                       hipStream_t s, const uint32_t* order) {

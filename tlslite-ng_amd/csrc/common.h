@@ -200,7 +200,10 @@ inline int device_cus() {
 // t of a lane-per-record kernel handles record order[t].
 int tg_launch_gcm(const tg::GcmKeyDev* key, int rounds, const tg_batch& b, bool open,
                   hipStream_t s, const uint32_t* order = nullptr);
-// The 8-block bitsliced single-key kernel (aes_gcm_bs8.hip).
+// The 8-block bitsliced single-key kernel and the hybrid T-table + bitsliced
+// persistent kernel (aes_gcm_bs8.hip).
+int tg_launch_gcm_hy(const tg::GcmKeyDev* key, int rounds, const tg_batch& b, bool open,
+                     hipStream_t s, const uint32_t* order);
 int tg_launch_gcm_bs8(const tg::GcmKeyDev* key, int rounds, const tg_batch& b, bool open,
                       hipStream_t s, const uint32_t* order);
 // hpow: the key table's GHASH powers (tg_launch_table_hpow), or NULL for the

@@ -65,6 +65,58 @@ __device__ __forceinline__ uint4 gmul_lowreg(uint4 y) {
     return z;
 }
 
+// Bank-conflict-free gmul (aes_gcm.hip GhashTablesRotLds): the tables in row
+// layout, entry (j, b) at b * 256 + j * 16, so the 16-byte bank slot of a
+// lookup is its table j; lane l walks the tables from j = l % 16, so the 16
+// lanes of every ds_read_b128 group hit 16 different slots whatever the data.
+// y is rotated by l % 16 bytes once per multiply; the four table-offset words
+// of lane l come from a 16-row LDS table at ``jt`` (row l % 16: byte k of word
+// q = ((l + 4 q + k) % 16) * 16).  lane16 = l % 16.  At most eight table rows
+// in flight (32 VGPRs).
+__device__ __forceinline__ uint4 gmul_rot(uint4 y, uint32_t lane16, uint32_t jt) {
+    const uint4 jw = lds_u128(jt + (lane16 << 4));
+    uint32_t u0 = y.x, u1 = y.y, u2 = y.z, u3 = y.w;
+    if (lane16 & 8u) { uint32_t t = u0; u0 = u2; u2 = t; t = u1; u1 = u3; u3 = t; }
+    if (lane16 & 4u) { uint32_t t = u0; u0 = u1; u1 = u2; u2 = u3; u3 = t; }
+    const uint32_t s8 = (lane16 & 3u) << 3;
+    const uint32_t v[4] = {__builtin_amdgcn_alignbit(u1, u0, s8), __builtin_amdgcn_alignbit(u2, u1, s8),
+                           __builtin_amdgcn_alignbit(u3, u2, s8), __builtin_amdgcn_alignbit(u0, u3, s8)};
+    const uint32_t j[4] = {jw.x, jw.y, jw.z, jw.w};
+    uint4 z = make_uint4(0, 0, 0, 0);
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        uint4 e[8];
+#pragma unroll
+        for (int t = 8 * h; t < 8 * h + 8; ++t) {
+            // byte 1 <- v[t/4] byte t%4 (the row b), byte 0 <- j[t/4] byte t%4
+            const uint32_t sel = 0x0c0c0000u | ((4u + (t & 3)) << 8) | (uint32_t)(t & 3);
+            e[t - 8 * h] = lds_u128(__builtin_amdgcn_perm(v[t >> 2], j[t >> 2], sel));
+        }
+        z = xor4_3(z, e[0], e[1]);
+        z = xor4_3(z, e[2], e[3]);
+        z = xor4_3(z, e[4], e[5]);
+        z = xor4_3(z, e[6], e[7]);
+    }
+    return z;
+}
+
+// Stage the 8-bit tables of ``src`` (GcmKeyDev layout, entry (j, b) at
+// j * 256 + b) in gmul_rot's row layout at LDS 0, and its lane-offset rows at
+// ``jt``.  Every thread of the workgroup calls it; a barrier must follow.
+__device__ __forceinline__ void stage_ghash_rot(uint4* lds, const uint4* __restrict__ src, uint32_t jt) {
+    for (int e = threadIdx.x; e < kGhashEntries; e += blockDim.x) lds[(e & 255) * 16 + (e >> 8)] = src[e];
+    if (threadIdx.x < 16) {
+        uint32_t w[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            w[q] = 0;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) w[q] |= (((threadIdx.x + 4 * q + k) & 15u) << 4) << (8 * k);
+        }
+        lds[jt / 16 + threadIdx.x] = make_uint4(w[0], w[1], w[2], w[3]);
+    }
+}
+
 // ---- table-free GHASH for key tables -----------------------------------
 // A key table cannot stage 64 KiB of GHASH tables per session, so each lane
 // multiplies by its own H with a carry-less multiply built from integer
