@@ -63,6 +63,8 @@ int tg_init(int device);                   /* hipSetDevice for the calling threa
  * tg_batch.key_idx (many sessions in one batch). */
 int tg_key_create(int alg, const uint8_t* keys, size_t keylen, size_t nkeys,
                   tg_key** out);
+/* tg_key_destroy waits for the device (batches on any stream may still read
+ * the key), then scrubs and frees the key material. */
 int tg_key_destroy(tg_key* k);
 int tg_key_info(const tg_key* k, int* alg, size_t* keylen, size_t* nkeys);
 
@@ -219,6 +221,27 @@ int64_t tg_scan_records(const uint8_t* buf, size_t len, uint32_t max_body, uint6
                         uint32_t* rlen, size_t max_n, size_t* consumed);
 int tg_gather(const uint8_t* src, const uint64_t* src_off, const uint32_t* len, uint8_t* dst,
               const uint64_t* dst_off, uint64_t n, void* stream);
+/* Self-test entry points (TEST-ONLY, not on the record path): run the
+ * engine's device Poly1305 / GHASH arithmetic on raw messages, HOST buffers,
+ * synchronous, so the reference's known answers reach the exact device code
+ * of the AEAD kernels (the reference's Poly1305 / GHASH have no entry point of
+ * their own: poly1305.py:32-48 Poly1305.create_tag, aesgcm.py:60-79
+ * AESGCM._auth with a zero tag mask).
+ * tg_selftest_poly1305: tags[i] = Poly1305(keys[i] (32 B), msgs + off[i],
+ *   len[i] bytes) with RFC padding; mode 0 = the lane Horner of the batch
+ *   kernel, 1 / 2 / 3 = the wave-striped Horner of the wave-per-record
+ *   kernel with 1 / 4 / 16 waves per message.
+ * tg_selftest_ghash: out[i] = GHASH_H(aad_i, ct_i) (h: n x 16 B, GCM byte
+ *   order); mode 0 = 8-bit tables, 1 = 8-bit tables 8 rows in flight,
+ *   2 = conflict-free rotated tables, 3 = table-free carry-less multiply,
+ *   4 = octet stride-H^8 + lift (aes_gcm_bs8.hip), 5 = wave stride-H^64 +
+ *   lift (gcm_wave_kernel). */
+int tg_selftest_poly1305(int mode, const uint8_t* keys, const uint8_t* msgs, const uint64_t* off,
+                         const uint32_t* len, uint64_t n, uint8_t* tags);
+int tg_selftest_ghash(int mode, const uint8_t* h, const uint8_t* aad, const uint64_t* aad_off,
+                      const uint32_t* aad_len, const uint8_t* ct, const uint64_t* ct_off,
+                      const uint32_t* ct_len, uint64_t n, uint8_t* out);
+
 /* Device memory helpers so a ctypes host needs no other GPU runtime. */
 int tg_malloc(void** p, size_t bytes);
 int tg_free(void* p);

@@ -1,8 +1,10 @@
-"""World-size-2 checks of the record sharding on CPU (gloo).
-
-Each rank seals its contiguous seq shard of one connection with the oracle
-(the GPU path is exercised by bench.py on real devices); concatenated per-rank
-output must equal a single-rank run, and the counter reduction must add up.
+"""World-size-2 checks of the record sharding on CPU (gloo), driving the same
+tlsgpu.distributed functions bench.py runs for N > 1: process setup, the weak
+shard plan (rank g seals seq [g n, (g+1) n)), the rank-offset nonces (host
+mirror of tg_make_nonces), the barrier-bracketed timed region, the counter
+reduction and the per-rank gather.  Each rank seals its shard with the oracle
+(the GPU kernels are the -m gpu tests' job); concatenated per-rank nonces and
+records must equal a single-rank run.
 """
 import hashlib
 import os
@@ -13,14 +15,14 @@ import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
 
-from tlsgpu.distributed import reduce_counters, shard_range, tls13_nonces
+from tlsgpu import distributed as tgd
 from vectors import tls13_aad, tls13_nonce
 
 
 def test_shard_range_partitions():
     for n in (0, 1, 7, 1 << 20, 1000003):
         for w in (1, 2, 3, 8):
-            spans = [shard_range(n, w, r) for r in range(w)]
+            spans = [tgd.shard_range(n, w, r) for r in range(w)]
             assert spans[0][0] == 0
             for (a, na), (b, _) in zip(spans, spans[1:]):
                 assert a + na == b
@@ -28,10 +30,40 @@ def test_shard_range_partitions():
             assert max(c for _, c in spans) - min(c for _, c in spans) <= 1
 
 
+def test_weak_shard_is_bench_plan():
+    for w in (1, 2, 4, 8):
+        spans = [tgd.weak_shard(1 << 20, w, r) for r in range(w)]
+        assert spans == [(r << 20, 1 << 20) for r in range(w)]
+    with pytest.raises(ValueError):
+        tgd.weak_shard(10, 2, 2)
+
+
 def test_host_nonces_match_record_layer():
     iv = bytes(range(12))
-    got = tls13_nonces(iv, 2 ** 33 - 2, 5)
+    got = tgd.tls13_nonces(iv, 2 ** 33 - 2, 5)
     assert got == b"".join(bytes(tls13_nonce(iv, 2 ** 33 - 2 + i)) for i in range(5))
+
+
+def test_nccl_needs_a_device_per_rank(monkeypatch):
+    """init_process refuses LOCAL_RANK >= device count under nccl instead of
+    wrapping several ranks onto one GPU."""
+    class FakeCuda(object):
+        @staticmethod
+        def device_count():
+            return 1
+
+        @staticmethod
+        def set_device(d):
+            raise AssertionError("must not be reached")
+
+    class FakeTorch(object):
+        cuda = FakeCuda()
+
+    monkeypatch.setenv("WORLD_SIZE", "2")
+    monkeypatch.setenv("RANK", "1")
+    monkeypatch.setenv("LOCAL_RANK", "1")
+    with pytest.raises(tgd.DistError):
+        tgd.init_process(FakeTorch(), None, backend="nccl")
 
 
 def _free_port():
@@ -42,42 +74,66 @@ def _free_port():
     return port
 
 
-N_TOTAL, LEN = 37, 300
+N_PER_RANK, LEN, STEPS = 19, 300, 2
+KEY, IV = bytes(range(32)), bytes(range(100, 112))
+
+
+def _pt(s):
+    return (hashlib.sha256(b"pt%d" % s).digest() * (LEN // 32 + 1))[:LEN]
 
 
 def _worker(rank, world, port, outdir):
-    os.environ["MASTER_ADDR"] = "127.0.0.1"
-    os.environ["MASTER_PORT"] = str(port)
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    os.environ.update({"MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port), "WORLD_SIZE": str(world),
+                       "RANK": str(rank), "LOCAL_RANK": str(rank)})
+    w, r, local, dev = tgd.init_process(torch, dist, backend="gloo", use_gpu=False)
+    assert (w, r, local, dev) == (world, rank, rank, None)
     import sys
     sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
     from oracle import oracle
-    key, iv = bytes(range(32)), bytes(range(100, 112))
-    first, count = shard_range(N_TOTAL, world, rank)
-    h = hashlib.sha256()
-    for s in range(first, first + count):
-        pt = hashlib.sha256(b"pt%d" % s).digest() * (LEN // 32 + 1)
-        out = oracle.chacha_seal(key, tls13_nonce(iv, s), pt[:LEN], tls13_aad(LEN))
-        h.update(bytes(out))
-        with open(os.path.join(outdir, "rec%05d" % s), "wb") as f:
-            f.write(bytes(out))
-    sums, tmax = reduce_counters(torch, dist, [count, count * LEN, 0], 0.1 * (rank + 1))
+    first, count = tgd.weak_shard(N_PER_RANK, world, rank)
+    nonces = tgd.tls13_nonces(IV, first, count)
+    out = {}
+
+    def step(k):
+        for i in range(count):
+            s = first + i
+            out[s] = bytes(oracle.chacha_seal(KEY, nonces[12 * i:12 * i + 12], _pt(s), tls13_aad(LEN)))
+
+    elapsed = tgd.timed(torch, dist, world, step, STEPS)
+    sums, tmax = tgd.reduce_counters(torch, dist, [count * STEPS, count * LEN * STEPS, 0], elapsed)
+    rows = tgd.gather_rows(torch, dist, [rank, count, first])
     with open(os.path.join(outdir, "rank%d" % rank), "w") as f:
-        f.write("%d %d %d %.3f" % (sums[0], sums[1], sums[2], tmax))
-    dist.barrier()
+        f.write("%d %d %d %.6f %.6f\n" % (sums[0], sums[1], sums[2], tmax, elapsed))
+        f.write(repr(rows) + "\n")
+    with open(os.path.join(outdir, "nonces%d" % rank), "wb") as f:
+        f.write(nonces)
+    for s, rec in out.items():
+        with open(os.path.join(outdir, "rec%05d" % s), "wb") as f:
+            f.write(rec)
+    tgd.barrier(torch, dist, world)
     dist.destroy_process_group()
 
 
 def test_world2_sharded_seal_equals_single(tmp_path):
     world = 2
     mp.spawn(_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
+    total = world * N_PER_RANK
+    tmaxes = []
     for r in range(world):
-        recs, payload, fails, tmax = open(tmp_path / ("rank%d" % r)).read().split()
-        assert int(recs) == N_TOTAL and int(payload) == N_TOTAL * LEN and int(fails) == 0
-        assert float(tmax) == pytest.approx(0.2)
+        lines = open(tmp_path / ("rank%d" % r)).read().splitlines()
+        recs, payload, fails, tmax, mine = lines[0].split()
+        assert int(float(recs)) == total * STEPS and int(float(payload)) == total * LEN * STEPS
+        assert int(float(fails)) == 0
+        assert float(tmax) >= float(mine)
+        tmaxes.append(float(tmax))
+        rows = eval(lines[1])   # noqa: S307 -- our own repr of a list of float lists
+        assert [int(x[0]) for x in rows] == list(range(world))
+        assert [int(x[2]) for x in rows] == [g * N_PER_RANK for g in range(world)]
+    assert tmaxes[0] == tmaxes[1]                       # every rank reports the max
+    # concatenated per-rank nonces == one rank covering all seqs
+    cat = b"".join(open(tmp_path / ("nonces%d" % r), "rb").read() for r in range(world))
+    assert cat == tgd.tls13_nonces(IV, 0, total)
     from oracle import oracle
-    key, iv = bytes(range(32)), bytes(range(100, 112))
-    for s in range(N_TOTAL):
-        pt = hashlib.sha256(b"pt%d" % s).digest() * (LEN // 32 + 1)
-        want = oracle.chacha_seal(key, tls13_nonce(iv, s), pt[:LEN], tls13_aad(LEN))
+    for s in range(total):
+        want = oracle.chacha_seal(KEY, tls13_nonce(IV, s), _pt(s), tls13_aad(LEN))
         assert open(tmp_path / ("rec%05d" % s), "rb").read() == bytes(want)

@@ -150,3 +150,20 @@ def test_tls13_all_zero_inner_plaintext(torch, tg):
     key, iv = bytes(16), bytes(12)
     _, opened = _run(torch, tg, "tls13", "aes128gcm", key, iv, 0, [0, 23], [b"", b"x"], [3, 0], True)
     assert opened[0][0] == 6 and opened[1] == (0, 23, b"x")
+
+
+@pytest.mark.parametrize("version,alg,ivlen", [("tls12", "aes128gcm", 12), ("tls12", "aes128ccm", 12),
+                                               ("tls13", "aes128gcm", 4),
+                                               ("tls13", "chacha20-poly1305", 4)])
+def test_fixed_iv_length_rejected(torch, tg, version, alg, ivlen):
+    """A fixed IV that gives no 12-byte nonce is an error, as the reference's
+    nonce-length assertion (recordlayer.py:522-534, :556): TLS 1.3 needs 12
+    bytes, TLS 1.2 AES-GCM / AES-CCM 4 (fixedNonce || seq)."""
+    import tlsgpu
+    klen = 32 if alg.startswith("chacha") else 16
+    k = _key(tg, alg, bytes(klen))
+    z = lambda n, dt=torch.uint8: torch.zeros(n, dtype=dt, device="cuda")  # noqa: E731
+    v = tg.TLS13 if version == "tls13" else tg.TLS12
+    with pytest.raises(tlsgpu.TlsGpuError):
+        tg.seal_records(k, v, bytes(ivlen), 0, 1, z(64), z(1, torch.int64), z(1, torch.int32),
+                        z(1), z(128), z(1, torch.int64), z(1, torch.int32))

@@ -148,3 +148,30 @@ def test_config1_digest(oracle_mod):
     for seq, pt in enumerate(pts):
         h.update(oracle_mod.chacha_seal(key, tls13_nonce(iv, seq), pt, tls13_aad(len(pt))))
     assert h.hexdigest() == BATCH["config1"]["sealed_sha256"]
+
+
+# ---- GHASH / Poly1305 edge vectors (tests/golden/make_golden_ghash.py) ----
+
+def test_ghash_golden_pyaead():
+    """pyaead's GHASH (the 4-bit-table restatement) against the reference's
+    AESGCM._auth values for edge-case H and lengths."""
+    gold = load("ghash.json")["ghash"]
+    for v in gold:
+        h = int.from_bytes(bytes.fromhex(v["h"]), "big")
+        tbl = pyaead._ghash_table(h)
+        aad = detbytes("ghash-aad-%d" % v["aad_len"], v["aad_len"])
+        ct = detbytes("ghash-ct-%d" % v["ct_len"], v["ct_len"])
+        y = pyaead._ghash(tbl, 0, aad)
+        y = pyaead._ghash(tbl, y, ct)
+        y = pyaead._gmul(tbl, y ^ ((len(aad) * 8) << 64 | len(ct) * 8))
+        assert y.to_bytes(16, "big").hex() == v["ghash"], (v["h_label"], v["aad_len"], v["ct_len"])
+
+
+def test_poly1305_golden_extra(oracle_mod):
+    """C and Python oracles against the reference's Poly1305 tags with r and s
+    at their clamped maxima over long all-0xff messages."""
+    for v in load("ghash.json")["poly1305_extra"]:
+        key = bytes.fromhex(v["key"])
+        msg = b"\xff" * v["len"] if v["msg_label"] == "ff" else bytes(detbytes(v["msg_label"], v["len"]))
+        assert bytes(pyaead.poly1305(key, msg)).hex() == v["tag"]
+        assert bytes(oracle_mod.poly1305(key, msg)).hex() == v["tag"]

@@ -371,8 +371,18 @@ int records(tg_key* k, const tg_records* r, void* stream, bool seal) {
     if (k->nkeys != 1) return fail(TG_EINVAL, "record framing needs a single-key handle");
     if (r->version != TG_TLS12 && r->version != TG_TLS13)
         return fail(TG_EINVAL, "version must be TG_TLS12 or TG_TLS13");
-    if (r->fixed_iv_len != 12 && !(r->fixed_iv_len == 4 && r->version == TG_TLS12))
-        return fail(TG_EINVAL, "fixed IV must be 12 bytes (or 4 for TLS 1.2)");
+    // _getNonce (recordlayer.py:522-534) then asserts a 12-byte nonce (:556):
+    // TLS 1.3 XORs a 12-byte IV; TLS 1.2 AES-GCM / AES-CCM append the 8-byte
+    // sequence number to a 4-byte IV; TLS 1.2 ChaCha XORs a 12-byte IV (RFC
+    // 7905) or appends to a 4-byte one (draft-00).
+    {
+        const bool chacha = k->alg == TG_CHACHA20_POLY1305;
+        const uint32_t ivl = r->fixed_iv_len;
+        const bool ok = r->version == TG_TLS13 ? ivl == 12 : chacha ? (ivl == 12 || ivl == 4) : ivl == 4;
+        if (!ok)
+            return fail(TG_EINVAL, "fixed IV of %u bytes gives no 12-byte nonce for this suite "
+                        "(TLS 1.3: 12; TLS 1.2 AES: 4; TLS 1.2 ChaCha: 12 or 4)", ivl);
+    }
     if (!r->data || !r->data_off || !r->data_len || !r->ctype || !r->wire || !r->wire_off ||
         !r->wire_len || (!seal && !r->status))
         return fail(TG_EINVAL, "null device array");
@@ -686,7 +696,11 @@ int tg_key_destroy(tg_key* k) {
     if (!k) return TG_OK;
     int cur = -1;
     if (hipGetDevice(&cur) == hipSuccess && cur != k->device) (void)hipSetDevice(k->device);
-    if (k->stream) (void)hipStreamSynchronize(k->stream);
+    // Batches may still be running on caller streams (tg_seal_batch and
+    // friends take any stream): wait for the whole device before the key
+    // material is scrubbed and released, so no launch ever reads a zeroed or
+    // freed schedule.
+    (void)hipDeviceSynchronize();
     if (k->dev_key) {
         // scrub key material before release
         (void)hipMemset(k->dev_key, 0, dev_key_bytes(k));

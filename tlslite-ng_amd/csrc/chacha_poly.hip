@@ -14,6 +14,7 @@
 #include <cstdlib>
 
 #include "common.h"
+#include "poly1305.h"
 
 namespace tg {
 namespace {
@@ -51,87 +52,6 @@ __device__ __forceinline__ void chacha_block(const uint32_t (&k)[8], uint32_t ct
     o[12] = x12 + ctr; o[13] = x13 + n0; o[14] = x14 + n1; o[15] = x15 + n2;
 }
 #undef QR
-
-// Poly1305 state in 26-bit limbs (value = sum h_i * 2^(26 i)).
-struct Poly {
-    uint32_t r0, r1, r2, r3, r4;
-    uint32_t s1, s2, s3, s4;  // 5 * r_i: 2^130 == 5 (mod 2^130 - 5)
-    uint32_t h0, h1, h2, h3, h4;
-    uint32_t p0, p1, p2, p3;  // s half of the one-time key
-};
-
-__device__ __forceinline__ void poly_init(Poly& p, const uint32_t (&otk)[16]) {
-    // r = LE(key[0:16]) & 0x0ffffffc0ffffffc0ffffffc0fffffff (poly1305.py:37-38)
-    p.r0 = otk[0] & 0x3ffffffu;
-    p.r1 = __builtin_amdgcn_alignbit(otk[1], otk[0], 26) & 0x3ffff03u;
-    p.r2 = __builtin_amdgcn_alignbit(otk[2], otk[1], 20) & 0x3ffc0ffu;
-    p.r3 = __builtin_amdgcn_alignbit(otk[3], otk[2], 14) & 0x3f03fffu;
-    p.r4 = (otk[3] >> 8) & 0x00fffffu;
-    p.s1 = p.r1 * 5; p.s2 = p.r2 * 5; p.s3 = p.r3 * 5; p.s4 = p.r4 * 5;
-    p.h0 = p.h1 = p.h2 = p.h3 = p.h4 = 0;
-    p.p0 = otk[4]; p.p1 = otk[5]; p.p2 = otk[6]; p.p3 = otk[7];
-}
-
-__device__ __forceinline__ uint64_t mul64(uint32_t a, uint32_t b) { return (uint64_t)a * b; }
-
-// acc = (acc + LE(m || 0x01)) * r mod 2^130-5 for one full 16-byte block
-// (poly1305.py:43-46).  mac_data is padded to 16 bytes (chacha20_poly1305.py:
-// 41-46), so every block carries the 2^128 bit.
-__device__ __forceinline__ void poly_block(Poly& p, uint4 m) {
-    const uint32_t M26 = 0x3ffffffu;
-    uint32_t h0 = p.h0 + (m.x & M26);
-    uint32_t h1 = p.h1 + (__builtin_amdgcn_alignbit(m.y, m.x, 26) & M26);
-    uint32_t h2 = p.h2 + (__builtin_amdgcn_alignbit(m.z, m.y, 20) & M26);
-    uint32_t h3 = p.h3 + (__builtin_amdgcn_alignbit(m.w, m.z, 14) & M26);
-    uint32_t h4 = p.h4 + ((m.w >> 8) | (1u << 24));
-    uint64_t d0 = mul64(h0, p.r0) + mul64(h1, p.s4) + mul64(h2, p.s3) + mul64(h3, p.s2) + mul64(h4, p.s1);
-    uint64_t d1 = mul64(h0, p.r1) + mul64(h1, p.r0) + mul64(h2, p.s4) + mul64(h3, p.s3) + mul64(h4, p.s2);
-    uint64_t d2 = mul64(h0, p.r2) + mul64(h1, p.r1) + mul64(h2, p.r0) + mul64(h3, p.s4) + mul64(h4, p.s3);
-    uint64_t d3 = mul64(h0, p.r3) + mul64(h1, p.r2) + mul64(h2, p.r1) + mul64(h3, p.r0) + mul64(h4, p.s4);
-    uint64_t d4 = mul64(h0, p.r4) + mul64(h1, p.r3) + mul64(h2, p.r2) + mul64(h3, p.r1) + mul64(h4, p.r0);
-    uint32_t c;
-    c = (uint32_t)(d0 >> 26); h0 = (uint32_t)d0 & M26;
-    d1 += c; c = (uint32_t)(d1 >> 26); h1 = (uint32_t)d1 & M26;
-    d2 += c; c = (uint32_t)(d2 >> 26); h2 = (uint32_t)d2 & M26;
-    d3 += c; c = (uint32_t)(d3 >> 26); h3 = (uint32_t)d3 & M26;
-    d4 += c; c = (uint32_t)(d4 >> 26); h4 = (uint32_t)d4 & M26;
-    h0 += c * 5; c = h0 >> 26; h0 &= M26;
-    h1 += c;
-    p.h0 = h0; p.h1 = h1; p.h2 = h2; p.h3 = h3; p.h4 = h4;
-}
-
-// tag = LE16((acc + s) mod 2^128) (poly1305.py:47-48)
-__device__ __forceinline__ uint4 poly_finish(const Poly& p) {
-    const uint32_t M26 = 0x3ffffffu;
-    uint32_t h0 = p.h0, h1 = p.h1, h2 = p.h2, h3 = p.h3, h4 = p.h4, c;
-    c = h1 >> 26; h1 &= M26; h2 += c;
-    c = h2 >> 26; h2 &= M26; h3 += c;
-    c = h3 >> 26; h3 &= M26; h4 += c;
-    c = h4 >> 26; h4 &= M26; h0 += c * 5;
-    c = h0 >> 26; h0 &= M26; h1 += c;
-    // g = h + 5 - 2^130; use g when h >= 2^130 - 5
-    uint32_t g0 = h0 + 5; c = g0 >> 26; g0 &= M26;
-    uint32_t g1 = h1 + c; c = g1 >> 26; g1 &= M26;
-    uint32_t g2 = h2 + c; c = g2 >> 26; g2 &= M26;
-    uint32_t g3 = h3 + c; c = g3 >> 26; g3 &= M26;
-    uint32_t g4 = h4 + c - (1u << 26);
-    uint32_t sel = (g4 >> 31) - 1u;  // all ones when no borrow
-    h0 = (h0 & ~sel) | (g0 & sel);
-    h1 = (h1 & ~sel) | (g1 & sel);
-    h2 = (h2 & ~sel) | (g2 & sel);
-    h3 = (h3 & ~sel) | (g3 & sel);
-    h4 = (h4 & ~sel) | (g4 & sel);
-    uint32_t w0 = h0 | (h1 << 26);
-    uint32_t w1 = (h1 >> 6) | (h2 << 20);
-    uint32_t w2 = (h2 >> 12) | (h3 << 14);
-    uint32_t w3 = (h3 >> 18) | (h4 << 8);
-    uint64_t f = (uint64_t)w0 + p.p0;
-    w0 = (uint32_t)f;
-    f = (uint64_t)w1 + p.p1 + (f >> 32); w1 = (uint32_t)f;
-    f = (uint64_t)w2 + p.p2 + (f >> 32); w2 = (uint32_t)f;
-    f = (uint64_t)w3 + p.p3 + (f >> 32); w3 = (uint32_t)f;
-    return make_uint4(w0, w1, w2, w3);
-}
 
 // The 64-byte blocks of a record.  Software-pipelined one block deep: while
 // block j is XORed and fed to Poly1305, the keystream of block j+1 is
@@ -349,60 +269,6 @@ __global__ __launch_bounds__(kChachaThreads, MINW) void chacha_kernel(
 // (square and multiply in the same 26-bit limbs) and the partials are summed
 // by a shuffle tree (and across the record's waves through LDS).  Thread 0
 // adds the AAD blocks (lifted by r^(nc+1)) and the length block (times r).
-struct F5 {
-    uint32_t h0, h1, h2, h3, h4;
-};
-
-// a * b mod 2^130 - 5, limbs of both < 2^26 (a little above for a's h1)
-__device__ __forceinline__ F5 fmul(const F5& a, const F5& b) {
-    const uint32_t M26 = 0x3ffffffu;
-    const uint32_t s1 = b.h1 * 5, s2 = b.h2 * 5, s3 = b.h3 * 5, s4 = b.h4 * 5;
-    uint64_t d0 = mul64(a.h0, b.h0) + mul64(a.h1, s4) + mul64(a.h2, s3) + mul64(a.h3, s2) + mul64(a.h4, s1);
-    uint64_t d1 = mul64(a.h0, b.h1) + mul64(a.h1, b.h0) + mul64(a.h2, s4) + mul64(a.h3, s3) + mul64(a.h4, s2);
-    uint64_t d2 = mul64(a.h0, b.h2) + mul64(a.h1, b.h1) + mul64(a.h2, b.h0) + mul64(a.h3, s4) + mul64(a.h4, s3);
-    uint64_t d3 = mul64(a.h0, b.h3) + mul64(a.h1, b.h2) + mul64(a.h2, b.h1) + mul64(a.h3, b.h0) + mul64(a.h4, s4);
-    uint64_t d4 = mul64(a.h0, b.h4) + mul64(a.h1, b.h3) + mul64(a.h2, b.h2) + mul64(a.h3, b.h1) + mul64(a.h4, b.h0);
-    F5 r;
-    uint32_t c;
-    c = (uint32_t)(d0 >> 26); r.h0 = (uint32_t)d0 & M26;
-    d1 += c; c = (uint32_t)(d1 >> 26); r.h1 = (uint32_t)d1 & M26;
-    d2 += c; c = (uint32_t)(d2 >> 26); r.h2 = (uint32_t)d2 & M26;
-    d3 += c; c = (uint32_t)(d3 >> 26); r.h3 = (uint32_t)d3 & M26;
-    d4 += c; c = (uint32_t)(d4 >> 26); r.h4 = (uint32_t)d4 & M26;
-    r.h0 += c * 5; c = r.h0 >> 26; r.h0 &= M26;
-    r.h1 += c;
-    return r;
-}
-
-__device__ __forceinline__ F5 fnorm_add(const F5& a, const F5& b) {
-    const uint32_t M26 = 0x3ffffffu;
-    F5 r = {a.h0 + b.h0, a.h1 + b.h1, a.h2 + b.h2, a.h3 + b.h3, a.h4 + b.h4};
-    uint32_t c;
-    c = r.h0 >> 26; r.h0 &= M26; r.h1 += c;
-    c = r.h1 >> 26; r.h1 &= M26; r.h2 += c;
-    c = r.h2 >> 26; r.h2 &= M26; r.h3 += c;
-    c = r.h3 >> 26; r.h3 &= M26; r.h4 += c;
-    c = r.h4 >> 26; r.h4 &= M26; r.h0 += c * 5;
-    c = r.h0 >> 26; r.h0 &= M26; r.h1 += c;
-    return r;
-}
-
-__device__ __forceinline__ F5 fpow(F5 x, uint32_t e) {
-    F5 r = {1, 0, 0, 0, 0};
-    while (e) {
-        if (e & 1) r = fmul(r, x);
-        e >>= 1;
-        if (e) x = fmul(x, x);
-    }
-    return r;
-}
-
-__device__ __forceinline__ F5 fshfl_xor(const F5& v, int m) {
-    return F5{(uint32_t)__shfl_xor((int)v.h0, m, 64), (uint32_t)__shfl_xor((int)v.h1, m, 64),
-              (uint32_t)__shfl_xor((int)v.h2, m, 64), (uint32_t)__shfl_xor((int)v.h3, m, 64),
-              (uint32_t)__shfl_xor((int)v.h4, m, 64)};
-}
-
 // W waves per record: W = 1 four records per 256-thread workgroup, W = 4 / 16
 // one record per 256 / 1024-thread workgroup (batches that leave CUs idle,
 // the per-record calls).
@@ -445,11 +311,7 @@ __global__ __launch_bounds__(chacha_wave_threads<W>()) void chacha_wave_kernel(
     F5 rgap = {0, 0, 0, 0, 0};
     uint32_t cb = 0;                                 // end of the thread's last block
     for (uint32_t q = lane; q < nq; q += S) {        // chacha20_poly1305.py:58-63
-        if (q != lane) {
-            if (q == lane + S) rgap = fpow(r, 4 * S - 4);   // only threads with a gap
-            const F5 h = fmul(F5{p.h0, p.h1, p.h2, p.h3, p.h4}, rgap);
-            p.h0 = h.h0; p.h1 = h.h1; p.h2 = h.h2; p.h3 = h.h3; p.h4 = h.h4;
-        }
+        stripe_gap<S>(p, r, q, lane, rgap);
         uint32_t ks[16];
         chacha_block(k, 1 + q, nv.x, nv.y, nv.z, ks);
 #pragma unroll
@@ -471,8 +333,7 @@ __global__ __launch_bounds__(chacha_wave_threads<W>()) void chacha_wave_kernel(
         cb = 4 * q + 4 < nc ? 4 * q + 4 : nc;
     }
     // lift: h r^(blocks after the thread's last one, incl. the length block)
-    F5 z = F5{p.h0, p.h1, p.h2, p.h3, p.h4};
-    if (cb) z = fmul(z, fpow(r, nc - cb + 1));
+    F5 z = stripe_lift(p, r, cb, nc - cb + 1);
     if (lane == 0) {
         Poly pa = p;                                 // the AAD (mac_data starts with it)
         pa.h0 = pa.h1 = pa.h2 = pa.h3 = pa.h4 = 0;
@@ -486,15 +347,7 @@ __global__ __launch_bounds__(chacha_wave_threads<W>()) void chacha_wave_kernel(
         poly_block(pl, make_uint4(alen, 0, len, 0));
         z = fnorm_add(z, F5{pl.h0, pl.h1, pl.h2, pl.h3, pl.h4});
     }
-#pragma unroll
-    for (int m = 1; m < 64; m <<= 1) z = fnorm_add(z, fshfl_xor(z, m));
-    if (W > 1) {
-        if ((lane & 63u) == 0) s_part[lane >> 6] = z;
-        __syncthreads();
-        z = s_part[0];
-#pragma unroll
-        for (int w = 1; w < W; ++w) z = fnorm_add(z, s_part[w]);
-    }
+    z = stripe_sum<W>(z, s_part, lane, 0);
     p.h0 = z.h0; p.h1 = z.h1; p.h2 = z.h2; p.h3 = z.h3; p.h4 = z.h4;
     const uint4 tag = poly_finish(p);                // poly1305.py:47-48
     const bool tag_aligned = aligned && (len & 15) == 0;

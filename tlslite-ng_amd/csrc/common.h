@@ -60,6 +60,41 @@ __host__ __device__ inline uint32_t gcm_word_to_norm(uint32_t w) {
     return r;
 }
 
+// Entry e = j * 256 + b of the 8-bit GHASH tables of G (hv: G as LE words of
+// its GCM bytes): b * x^(8j) * G in the same layout (aesgcm.py:8-14 bit order,
+// _mul :86-97 restated bitwise).  Built on the device by keysetup.hip and by
+// the self-test (selftest.hip); api.hip's host builder gives the same tables.
+__host__ __device__ inline uint4 ghash_table_entry(const uint32_t hv[4], int e) {
+    const int j = e >> 8, b = e & 255;
+    uint64_t hi = 0, lo = 0;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) hi = (hi << 8) | ((hv[k >> 2] >> (8 * (k & 3))) & 0xff);
+#pragma unroll
+    for (int k = 8; k < 16; ++k) lo = (lo << 8) | ((hv[k >> 2] >> (8 * (k & 3))) & 0xff);
+    uint64_t zh = 0, zl = 0;
+    for (int nsh = 0; nsh < 8 * j + 8; ++nsh) {             // V = H * x^nsh
+        if (nsh >= 8 * j && (b & (0x80 >> (nsh - 8 * j)))) {
+            zh ^= hi;
+            zl ^= lo;
+        }
+        const uint64_t carry = lo & 1;
+        lo = (lo >> 1) | (hi << 63);
+        hi >>= 1;
+        if (carry) hi ^= 0xe1ull << 56;
+    }
+    uint32_t w[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const uint64_t half = q < 2 ? zh : zl;
+        const int sh = q & 1 ? 24 : 56;
+        uint32_t v = 0;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) v |= (uint32_t)((half >> (sh - 8 * k)) & 0xff) << (8 * k);
+        w[q] = v;
+    }
+    return make_uint4(w[0], w[1], w[2], w[3]);
+}
+
 // Entry e of GcmKeyDev::bsmask from the round-key words.
 __host__ __device__ inline uint32_t bs_mask_word(const uint32_t* rk, int e) {
     const int r = e >> 7, k = (e >> 3) & 15, bit = e & 7;

@@ -323,36 +323,6 @@ __global__ void aes_setup_kernel(const uint8_t* __restrict__ keys, uint64_t n, v
 // block byte layout (api.hip build_ghash_tables; aesgcm.py:8-14 bit order).
 // Entry (0, 0) = 0 holds H on entry and is left alone here (every thread reads
 // it); the launcher zeroes it afterwards, stream-ordered.
-__device__ __forceinline__ uint4 ghash_table_entry(const uint32_t hv[4], int e) {
-    const int j = e >> 8, b = e & 255;
-    uint64_t hi = 0, lo = 0;
-#pragma unroll
-    for (int k = 0; k < 8; ++k) hi = (hi << 8) | ((hv[k >> 2] >> (8 * (k & 3))) & 0xff);
-#pragma unroll
-    for (int k = 8; k < 16; ++k) lo = (lo << 8) | ((hv[k >> 2] >> (8 * (k & 3))) & 0xff);
-    uint64_t zh = 0, zl = 0;
-    for (int nsh = 0; nsh < 8 * j + 8; ++nsh) {             // V = H * x^nsh
-        if (nsh >= 8 * j && (b & (0x80 >> (nsh - 8 * j)))) {
-            zh ^= hi;
-            zl ^= lo;
-        }
-        const uint64_t carry = lo & 1;
-        lo = (lo >> 1) | (hi << 63);
-        hi >>= 1;
-        if (carry) hi ^= 0xe1ull << 56;
-    }
-    uint32_t w[4];
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-        const uint64_t half = q < 2 ? zh : zl;
-        const int sh = q & 1 ? 24 : 56;
-        uint32_t v = 0;
-#pragma unroll
-        for (int k = 0; k < 4; ++k) v |= (uint32_t)((half >> (sh - 8 * k)) & 0xff) << (8 * k);
-        w[q] = v;
-    }
-    return make_uint4(w[0], w[1], w[2], w[3]);
-}
 
 __global__ void ghash_table_kernel(GcmKeyDev* key) {
     const int e = blockIdx.x * blockDim.x + threadIdx.x;   // entry j * 256 + b

@@ -30,7 +30,8 @@ EXPORTS = ("tg_version", "tg_last_error", "tg_device_count", "tg_init", "tg_key_
            "tg_key_destroy", "tg_key_info", "tg_key_taglen", "tg_seal", "tg_open", "tg_seal_batch",
            "tg_open_batch", "tg_make_nonces", "tg_malloc", "tg_free", "tg_memcpy_h2d",
            "tg_memcpy_d2h", "tg_stream_sync", "tg_seal_records", "tg_open_records",
-           "tg_hkdf_expand_label", "tg_key_create_device", "tg_scan_records", "tg_gather")
+           "tg_hkdf_expand_label", "tg_key_create_device", "tg_scan_records", "tg_gather",
+           "tg_selftest_poly1305", "tg_selftest_ghash")
 
 TG_TLS12 = 0x0303
 TG_TLS13 = 0x0304
@@ -129,6 +130,8 @@ def load():
     l.tg_stream_sync.argtypes = [p]
     l.tg_scan_records.argtypes = [p, sz, ctypes.c_uint32, p, p, sz, ctypes.POINTER(sz)]
     l.tg_gather.argtypes = [p, p, p, p, p, u64, p]
+    l.tg_selftest_poly1305.argtypes = [i, p, p, p, p, u64, p]
+    l.tg_selftest_ghash.argtypes = [i, p, p, p, p, p, p, p, u64, p]
     for name in EXPORTS:
         if name not in ("tg_version", "tg_last_error"):
             getattr(l, name).restype = ctypes.c_int

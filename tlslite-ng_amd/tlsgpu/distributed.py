@@ -3,11 +3,54 @@
 A connection's records are independent AEAD calls keyed by (key, fixed IV,
 seq) -- tlslite/recordlayer.py:251-256 (seq), :522-534 (nonce) -- so a batch
 shards by contiguous sequence-number range with no data exchange: rank r of W
-seals seq [seq0_r, seq0_r + n_r).  The only collective is a reduction of the
-per-rank counters (records, payload bytes, auth failures) and of the timing
-max, which bench.py runs over RCCL (backend "nccl") on GPUs and the tests run
-over gloo on CPU.
+seals seq [seq0_r, seq0_r + n_r).  The only collectives are reductions of the
+per-rank counters (records, payload bytes, auth failures), of the timing max,
+and a gather of the per-rank kernel rates for the report -- bench.py runs them
+over RCCL (backend "nccl") on GPUs, tests/test_distributed.py over gloo on CPU.
+
+Everything bench.py does for N > 1 lives here (process setup, the shard plan,
+the per-rank nonces, the barrier-bracketed timed region, the reductions), so
+the world-size-2 CPU test drives the same functions.
 """
+import os
+import time
+
+
+class DistError(RuntimeError):
+    pass
+
+
+def env_rank():
+    """(world, rank, local_rank) from the torch.distributed.run environment."""
+    return (int(os.environ.get("WORLD_SIZE", "1")), int(os.environ.get("RANK", "0")),
+            int(os.environ.get("LOCAL_RANK", "0")))
+
+
+def init_process(torch, dist, backend=None, use_gpu=True):
+    """One process per GPU.  backend None = TLSGPU_DIST_BACKEND or "nccl"
+    (= RCCL over xGMI on ROCm).  Under nccl every rank needs its own device:
+    LOCAL_RANK >= device count is an error (no silent oversubscription).  gloo
+    is the CPU rehearsal backend; with use_gpu it may map several ranks to one
+    device (rank % device count), which is only for rehearsals.
+    Returns (world, rank, local_rank, device or None)."""
+    world, rank, local = env_rank()
+    backend = backend or os.environ.get("TLSGPU_DIST_BACKEND", "nccl")
+    device = None
+    if use_gpu:
+        ndev = torch.cuda.device_count()
+        if ndev < 1:
+            raise DistError("no GPU visible")
+        if backend == "nccl" and local >= ndev:
+            raise DistError("LOCAL_RANK %d >= %d visible GPUs: one process per GPU needs a device "
+                            "per local rank" % (local, ndev))
+        device = local if backend == "nccl" else local % ndev
+        torch.cuda.set_device(device)
+    if world > 1:
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", device))
+        else:
+            dist.init_process_group(backend)
+    return world, rank, local, device
 
 
 def shard_range(n_total, world, rank):
@@ -17,6 +60,14 @@ def shard_range(n_total, world, rank):
     base, extra = divmod(int(n_total), int(world))
     first = rank * base + min(rank, extra)
     return first, base + (1 if rank < extra else 0)
+
+
+def weak_shard(n_per_rank, world, rank, seq_base=0):
+    """Weak scaling (bench.py, BASELINE configs[4]): every rank seals
+    ``n_per_rank`` records, rank g the seqs [g n, (g + 1) n).  (first, count)."""
+    if world < 1 or not 0 <= rank < world:
+        raise ValueError("bad rank/world")
+    return seq_base + rank * int(n_per_rank), int(n_per_rank)
 
 
 def tls13_nonces(iv, seq0, n):
@@ -29,6 +80,37 @@ def tls13_nonces(iv, seq0, n):
     return bytes(out)
 
 
+def shard_nonces(tlsgpu, iv, first, count, out):
+    """This rank's nonces on the device (tg_make_nonces with the rank's seq
+    offset); tls13_nonces(iv, first, count) is the host mirror."""
+    tlsgpu.make_nonces(iv, first, count, out)
+    return out
+
+
+def _sync(torch):
+    if torch.cuda.is_available() and torch.cuda.is_initialized():
+        torch.cuda.synchronize()
+
+
+def barrier(torch, dist, world):
+    """Device sync, then (N > 1) a process barrier, then device sync."""
+    _sync(torch)
+    if world > 1:
+        dist.barrier()
+    _sync(torch)
+
+
+def timed(torch, dist, world, fn, steps):
+    """The bench contract's timed region: barrier + device sync on both sides
+    of exactly ``steps`` calls of ``fn(step)``; returns this rank's seconds."""
+    barrier(torch, dist, world)
+    t0 = time.perf_counter()
+    for s in range(steps):
+        fn(s)
+    barrier(torch, dist, world)
+    return time.perf_counter() - t0
+
+
 def reduce_counters(torch, dist, counters, elapsed, device=None):
     """Sum ``counters`` (list of numbers) and take the max of ``elapsed`` over
     all ranks.  Returns (summed list, max elapsed)."""
@@ -38,3 +120,14 @@ def reduce_counters(torch, dist, counters, elapsed, device=None):
         dist.all_reduce(c, op=dist.ReduceOp.SUM)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return [float(x) for x in c.tolist()], float(t.item())
+
+
+def gather_rows(torch, dist, row, device=None):
+    """All ranks' ``row`` (list of numbers, same length everywhere) as a list
+    of lists indexed by rank (the per-rank kernel rates of the report)."""
+    t = torch.tensor([float(x) for x in row], dtype=torch.float64, device=device)
+    if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+        out = [torch.zeros_like(t) for _ in range(dist.get_world_size())]
+        dist.all_gather(out, t)
+        return [[float(x) for x in o.tolist()] for o in out]
+    return [[float(x) for x in t.tolist()]]

@@ -1,11 +1,22 @@
-"""HBM bytes per launch of the headline kernels from tools/traffic.sh output.
+"""HBM bytes per launch of the headline kernels from tools/traffic.sh output,
+calibrated per access shape.
 
-Corrections (MI355X_MICROARCH.md, HBM section): rocprofv3 FETCH_SIZE and
-WRITE_SIZE are in KB (1024 B); on gfx950 FETCH_SIZE reports half the bytes of
-a wide streaming read (128-B requests tallied at 64 B), so it is doubled;
-WRITE_SIZE is taken as is.  Both count memory-side (fabric) requests, i.e.
-Infinity-Cache hits are included; the headline working set (32 GiB) is far
-past the 256 MiB Infinity Cache.
+rocprofv3 FETCH_SIZE / WRITE_SIZE are in KB (1024 B) and count memory-side
+(fabric) requests.  On gfx950 their relation to the bytes moved depends on
+the access shape (MI355X_MICROARCH.md: FETCH_SIZE reports half the bytes of a
+wide coalesced streaming read; other widths are uncalibrated).  So
+tools/fetch_calib.hip copies exactly 4 GiB with each shape the kernels use,
+under the same counter passes, and the factor of a shape is
+bytes / counter bytes; a kernel's traffic is its raw counters times the
+factors of its shape:
+
+  aes128gcm_*        gcm_hy_kernel (octet: 8 records x 128 B per instruction)
+  chacha20-poly1305_* chacha_kernel (tile64: 16 records x 64 B per instruction)
+
+The headline working set (48 GiB) is far past the 256 MiB Infinity Cache, so
+cache hits in the counters are negligible.
+
+    python tools/traffic_summary.py <traffic.sh output dir>  > traffic.json
 """
 import csv
 import glob
@@ -15,33 +26,50 @@ import re
 import sys
 from collections import defaultdict
 
-NAMES = [(r"gcm_kernel<10, false", "aes128gcm_seal"), (r"gcm_kernel<10, true", "aes128gcm_open"),
-         (r"chacha_kernel<false", "chacha20-poly1305_seal"),
-         (r"chacha_kernel<true", "chacha20-poly1305_open")]
+CAL_BYTES = 16384 * (1 << 18)
+CAL = {"k_coalesced": "coalesced", "k_octet": "octet", "k_tile64": "tile64", "k_lane": "lane"}
+KERNELS = [(r"gcm_hy_kernel<10, false", "aes128gcm_seal", "octet"),
+           (r"gcm_hy_kernel<10, true", "aes128gcm_open", "octet"),
+           (r"chacha_kernel<false", "chacha20-poly1305_seal", "tile64"),
+           (r"chacha_kernel<true", "chacha20-poly1305_open", "tile64")]
 
 
-def label(name):
-    for pat, lab in NAMES:
-        if re.search(pat, name):
-            return lab
-    return None
+def collect(d, pattern):
+    vals = defaultdict(lambda: defaultdict(list))
+    for f in glob.glob(os.path.join(d, pattern, "**", "*counter_collection.csv"), recursive=True):
+        for row in csv.DictReader(open(f)):
+            vals[row.get("Kernel_Name", "")][row["Counter_Name"]].append(float(row["Counter_Value"]))
+    return vals
+
+
+def mean_kb(lst):
+    return sum(lst) / max(len(lst), 1) * 1024
 
 
 def main(d):
-    vals = defaultdict(lambda: defaultdict(list))
-    for f in glob.glob(os.path.join(d, "*", "**", "*counter_collection.csv"), recursive=True):
-        for row in csv.DictReader(open(f)):
-            lab = label(row.get("Kernel_Name", ""))
-            if lab:
-                vals[lab][row["Counter_Name"]].append(float(row["Counter_Value"]))
+    cal_raw = collect(d, "cal_*")
+    factors = {}
+    for name, c in cal_raw.items():
+        for k, shape in CAL.items():
+            if re.search(r"\b%s\b" % k, name):
+                fetch, write = mean_kb(c["FETCH_SIZE"]), mean_kb(c["WRITE_SIZE"])
+                factors[shape] = {"fetch_size_bytes": fetch, "write_size_bytes": write,
+                                  "fetch_factor": round(CAL_BYTES / fetch, 4) if fetch else None,
+                                  "write_factor": round(CAL_BYTES / write, 4) if write else None}
+    raw = collect(d, "bench_*")
     out = {}
-    for lab, c in vals.items():
-        fetch = sum(c["FETCH_SIZE"]) / max(len(c["FETCH_SIZE"]), 1) * 1024
-        write = sum(c["WRITE_SIZE"]) / max(len(c["WRITE_SIZE"]), 1) * 1024
-        out[lab] = {"fetch_size_bytes": fetch, "write_size_bytes": write,
-                    "hbm_read_bytes": 2 * fetch, "hbm_write_bytes": write,
-                    "hbm_bytes": 2 * fetch + write, "launches": len(c["FETCH_SIZE"])}
-    print(json.dumps(out, indent=1, sort_keys=True))
+    for name, c in raw.items():
+        for pat, lab, shape in KERNELS:
+            if re.search(pat, name) and shape in factors:
+                fetch, write = mean_kb(c["FETCH_SIZE"]), mean_kb(c["WRITE_SIZE"])
+                ff, wf = factors[shape]["fetch_factor"], factors[shape]["write_factor"]
+                out[lab] = {"fetch_size_bytes": fetch, "write_size_bytes": write, "shape": shape,
+                            "fetch_factor": ff, "write_factor": wf,
+                            "hbm_read_bytes": fetch * ff, "hbm_write_bytes": write * wf,
+                            "hbm_bytes": fetch * ff + write * wf,
+                            "launches": len(c["FETCH_SIZE"])}
+    print(json.dumps({"calibration": factors, "calibration_bytes": CAL_BYTES, "kernels": out},
+                     indent=1, sort_keys=True))
 
 
 if __name__ == "__main__":
