@@ -158,13 +158,17 @@ int tg_make_nonces(int mode, const uint8_t* iv, size_t ivlen, uint64_t seq0,
 #define TG_REC_BAD_TYPE 4       /* TLSUnexpectedMessage, encrypted non-app-data (:809-812) */
 #define TG_REC_BAD_VERSION 5    /* TLSIllegalParameterException (:813-815) */
 #define TG_REC_NO_CONTENT_TYPE 6 /* malformed inner plaintext (:880-882) */
+#define TG_REC_OVERFLOW 7       /* TLSRecordOverflow: header length over the limit
+                                   (RecordSocket.recv :219-222), TLS 1.3 inner
+                                   plaintext over limit + 1 (:974-975), plaintext
+                                   over limit (:980-981) */
 
 typedef struct tg_records {
     uint64_t n;
     uint32_t version;           /* TG_TLS12 or TG_TLS13 */
     uint32_t fixed_iv_len;      /* 4 (TLS 1.2 AES-GCM / AES-CCM) or 12 */
     uint8_t fixed_iv[12];
-    uint32_t reserved;
+    uint32_t recv_limit;        /* open: recv_record_limit (0 = 2^14, recordlayer.py:56) */
     uint64_t seq0;
     uint8_t* data;
     const uint64_t* data_off;

@@ -3,13 +3,15 @@
 Checker for tg_seal_records / tg_open_records.  Follows
 tlslite/recordlayer.py: _getNonce :522-534, _encryptThenSeal :536-565,
 sendRecord :606-617 (TLS 1.3 inner plaintext), _decryptAndUnseal :780-824,
-_tls13_de_pad :863-884.  Pinned against tests/golden/records.json, which
+_tls13_de_pad :863-884, and the record-size limits of RecordSocket.recv
+:219-222 and recvRecord :974-981 (TLSRecordOverflow).  Pinned against tests/golden/records.json, which
 the reference RecordLayer itself produced (tests/golden/make_golden_records.py).
 Status codes are include/tlsgpu.h TG_REC_*.
 """
 from . import oracle
 
-OK, BAD_MAC, TRUNCATED, LENGTH, BAD_TYPE, BAD_VERSION, NO_CONTENT_TYPE = range(7)
+OK, BAD_MAC, TRUNCATED, LENGTH, BAD_TYPE, BAD_VERSION, NO_CONTENT_TYPE, OVERFLOW = range(8)
+RECV_LIMIT = 2 ** 14   # recv_record_limit (recordlayer.py:56)
 APP_DATA = 23
 
 
@@ -50,13 +52,16 @@ def seal_record(version, alg, key, iv, seq, ctype, data, pad=0):
     return bytes([ctype, 3, 3, len(body) >> 8, len(body) & 0xff]) + body
 
 
-def open_record(version, alg, key, iv, seq, wire):
+def open_record(version, alg, key, iv, seq, wire, limit=RECV_LIMIT):
     """-> (status, content type, plaintext)"""
     _, open_ = _pair(alg)
     wire = bytes(wire)
     if len(wire) < 5:
         return TRUNCATED, 0, b""
     hdr, buf = wire[:5], wire[5:]
+    # RecordSocket.recv refuses the header first (recordlayer.py:219-222)
+    if len(buf) > limit + 2048 or (version == "tls13" and len(buf) > limit + 256):
+        return OVERFLOW, 0, b""
     explicit = 8 if (version == "tls12" and not alg.startswith("chacha")) else 0
     if explicit > len(buf):
         return TRUNCATED, 0, b""
@@ -83,7 +88,11 @@ def open_record(version, alg, key, iv, seq, wire):
         return BAD_MAC, 0, b""
     pt = bytes(pt)
     if version == "tls12":
+        if len(pt) > limit:                               # :980-981
+            return OVERFLOW, 0, b""
         return OK, hdr[0], pt
+    if len(pt) > limit + 1:                               # :974-975
+        return OVERFLOW, 0, b""
     pos = len(pt)
     while pos > 0 and pt[pos - 1] == 0:
         pos -= 1

@@ -76,14 +76,17 @@ def test_writer_vs_oracle_and_reader_roundtrip(torch, tg, ver, alg, klen, ivlen)
     iv = detbytes("ingest-iv-" + alg, ivlen)
     version = tg.TLS13 if ver == "tls13" else tg.TLS12
     pad = 3 if ver == "tls13" else 0
+    # fragments shortened by the padding: the inner plaintext stays within
+    # the 2^14 + 1 the receiver accepts (recordlayer.py:974-975)
+    limit = 2 ** 14 - pad
     sink = Sink()
     w = tg.RecordWriter(sink, _key(tg, alg, key), version, iv, seq0=5, batch_records=7,
-                        pad=pad)
+                        pad=pad, send_record_limit=limit)
     msgs = _messages(klen + ivlen)
     for m in msgs:
         w.write(m)
     w.flush()
-    frags = _fragments(msgs, 2 ** 14)
+    frags = _fragments(msgs, limit)
     want = b"".join(orec.seal_record(ver, alg, key, iv, 5 + i, 23, f, pad=pad)
                     for i, f in enumerate(frags))
     assert w.records_sent == len(frags)
@@ -149,3 +152,20 @@ def test_socketpair_bulk(torch, tg):
     a.close()
     b.close()
     assert out == data
+
+
+def test_reader_refuses_oversized_inner_plaintext(torch, tg):
+    """A TLS 1.3 record whose inner plaintext exceeds 2^14 + 1 (a full 2^14
+    fragment with padding) is refused with TLSRecordOverflow after the
+    records before it, as the reference's recvRecord does
+    (recordlayer.py:974-975; tests/golden/records.json "recv")."""
+    from tlsgpu.ingest import TLSRecordOverflow
+    key, iv = detbytes("ingest-ovf", 16), detbytes("ingest-ovf-iv", 12)
+    recs = [orec.seal_record("tls13", "aes128gcm", key, iv, i, 23, detbytes("o%d" % i, 16384),
+                             pad=(3 if i == 2 else 0)) for i in range(4)]
+    r = tg.RecordReader(_key(tg, "aesgcm", key), tg.TLS13, iv)
+    r.feed(b"".join(recs))
+    ok = r.records()
+    assert [bytes(d) for _, d in ok] == [bytes(detbytes("o%d" % i, 16384)) for i in range(2)]
+    with pytest.raises(TLSRecordOverflow):
+        r.records()

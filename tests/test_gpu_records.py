@@ -112,7 +112,10 @@ def test_reference_wire_bytes(torch, tg, ci, aligned):
     for r, w, d, o in zip(recs, wires, datas, opened):
         assert len(w) == r["wire_len"]
         assert hashlib.sha256(w).hexdigest() == r["wire_sha256"], (c["version"], c["alg"])
-        assert o == (0, r["ctype"], d)
+        if r.get("recv", "ok") == "ok":
+            assert o == (0, r["ctype"], d)
+        else:   # the reference receiver raised TLSRecordOverflow (recordlayer.py:974-975)
+            assert r["recv"] == "TLSRecordOverflow" and o[0] == 7, (c["version"], c["alg"], r["len"])
 
 
 @pytest.mark.parametrize("version,alg,klen,ivlen", [
@@ -167,3 +170,21 @@ def test_fixed_iv_length_rejected(torch, tg, version, alg, ivlen):
     with pytest.raises(tlsgpu.TlsGpuError):
         tg.seal_records(k, v, bytes(ivlen), 0, 1, z(64), z(1, torch.int64), z(1, torch.int32),
                         z(1), z(128), z(1, torch.int64), z(1, torch.int32))
+
+
+def test_record_limits_device(torch, tg):
+    """TLSRecordOverflow cases on the device, as the framing oracle
+    (recordlayer.py:219-222, :974-981): a TLS 1.3 record over 2^14 + 256 bytes
+    (header), a TLS 1.3 inner plaintext of 2^14 + 2, a TLS 1.2 plaintext of
+    2^14 + 1; the full 2^14 records beside them open."""
+    from oracle import records as R
+    key, iv = bytes(range(16)), bytes(range(12))
+    datas = [bytes(16384), bytes(16384), bytes(16384), bytes(100)]
+    pads = [0, 1, 300, 0]
+    wires, opened = _run(torch, tg, "tls13", "aes128gcm", key, iv, 5, [23] * 4, datas, pads, True)
+    assert [o[0] for o in opened] == [0, 7, 7, 0]
+    for i in range(4):
+        assert R.open_record("tls13", "aes128gcm", key, iv, 5 + i, wires[i])[0] == opened[i][0]
+    wires, opened = _run(torch, tg, "tls12", "aes128gcm", key, iv[:4], 9, [23, 23],
+                         [bytes(16385), bytes(16384)], [0, 0], True)
+    assert [o[0] for o in opened] == [7, 0]

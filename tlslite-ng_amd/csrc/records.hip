@@ -100,6 +100,10 @@ __global__ void open_prep(tg_records r, bool aes, uint32_t taglen, RecScratch s)
     if (wl < 5 || explicit_len > buf_len) st = TG_REC_TRUNCATED;           // :787-789
     else if (buf_len - explicit_len < taglen) st = TG_REC_TRUNCATED;       // :797-799
     const uint8_t type = wl >= 1 ? w[0] : 0;
+    const uint32_t limit = r.recv_limit ? r.recv_limit : 16384u;
+    // RecordSocket.recv (:219-222) refuses the header before any decryption
+    if (st == TG_REC_OK && (buf_len > limit + 2048u || (tls13 && buf_len > limit + 256u)))
+        st = TG_REC_OVERFLOW;
     if (st == TG_REC_OK && tls13) {
         const uint32_t ver = ((uint32_t)w[1] << 8) | w[2];
         const uint32_t hlen = ((uint32_t)w[3] << 8) | w[4];
@@ -143,6 +147,8 @@ __global__ void open_finish(tg_records r, RecScratch s) {
     if (st == TG_REC_OK && s.aead_st[i] != 1) st = TG_REC_BAD_MAC;         // :822-823
     uint32_t plen = 0;
     uint8_t type = 0;
+    const uint32_t limit = r.recv_limit ? r.recv_limit : 16384u;
+    if (st == TG_REC_OK && tls13 && s.len[i] > limit + 1u) st = TG_REC_OVERFLOW;   // :974-975
     if (st == TG_REC_OK) {
         const uint32_t ct_len = s.len[i];
         if (tls13) {  // last non-zero byte is the content type (:863-884)
@@ -159,6 +165,7 @@ __global__ void open_finish(tg_records r, RecScratch s) {
             type = r.wire[r.wire_off[i]];
             plen = ct_len;
         }
+        if (st == TG_REC_OK && plen > limit) st = TG_REC_OVERFLOW;                  // :980-981
     }
     r.data_len[i] = plen;
     r.ctype[i] = type;

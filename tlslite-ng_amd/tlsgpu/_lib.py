@@ -37,7 +37,8 @@ TG_TLS12 = 0x0303
 TG_TLS13 = 0x0304
 # per-record status of tg_open_records (include/tlsgpu.h TG_REC_*)
 REC_STATUS = {0: "ok", 1: "bad_record_mac", 2: "truncated", 3: "length_mismatch",
-              4: "unexpected_content_type", 5: "illegal_version", 6: "no_content_type"}
+              4: "unexpected_content_type", 5: "illegal_version", 6: "no_content_type",
+              7: "record_overflow"}
 
 
 class TgBatch(ctypes.Structure):
@@ -70,7 +71,7 @@ class TgRecords(ctypes.Structure):
         ("version", ctypes.c_uint32),
         ("fixed_iv_len", ctypes.c_uint32),
         ("fixed_iv", ctypes.c_uint8 * 12),
-        ("reserved", ctypes.c_uint32),
+        ("recv_limit", ctypes.c_uint32),
         ("seq0", ctypes.c_uint64),
         ("data", ctypes.c_void_p),
         ("data_off", ctypes.c_void_p),

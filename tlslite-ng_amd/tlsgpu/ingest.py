@@ -61,6 +61,7 @@ _STATUS_EXC = {
     4: (TLSUnexpectedMessage, "Invalid ContentType for encrypted record"),
     5: (TLSIllegalParameterException, "Unexpected version in encrypted record"),
     6: (TLSUnexpectedMessage, "Malformed record layer inner plaintext - content type missing"),
+    7: (TLSRecordOverflow, "Record over the receive limit"),
 }
 
 APPLICATION_DATA = 23
@@ -255,6 +256,7 @@ class RecordReader(object):
         self.fixed_iv = bytes(fixed_iv)
         self.seq = int(seq0)
         # RecordSocket.recv (:217-222): 2**14 + 2048 always, 2**14 + 256 for TLS 1.3
+        self.recv_record_limit = int(recv_record_limit)
         self.max_body = recv_record_limit + (256 if version == TLS13 else 2048)
         self.batch = int(batch_records)
         self.hdr = 5 + _explicit_nonce(version, key)
@@ -404,7 +406,7 @@ class RecordReader(object):
             gather(s.d_pack, self.d_src, self.d_rl, s.d_wire, s.d_wire_off, n, stream=s.stream)
             open_records(self.key, self.version, self.fixed_iv, self.seq, n, s.d_wire,
                          s.d_wire_off, self.d_rl, s.d_data, s.d_data_off, s.d_len, s.d_ctype,
-                         s.d_status, stream=s.stream)
+                         s.d_status, stream=s.stream, recv_limit=self.recv_record_limit)
             self.h_plen[:n].copy_(s.d_len[:n], non_blocking=True)
             s.h_ctype[:n].copy_(s.d_ctype[:n], non_blocking=True)
             s.h_status[:n].copy_(s.d_status[:n], non_blocking=True)

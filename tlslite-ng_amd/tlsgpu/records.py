@@ -27,9 +27,10 @@ STATUS = _lib.REC_STATUS
 
 
 def _records(n, version, fixed_iv, seq0, data, data_off, data_len, ctype, wire, wire_off,
-             wire_len, pad_len=None, status=None):
+             wire_len, pad_len=None, status=None, recv_limit=0):
     r = _lib.TgRecords()
     r.n = int(n)
+    r.recv_limit = int(recv_limit)
     r.version = int(version)
     iv = bytes(fixed_iv)
     if len(iv) not in (4, 12):
@@ -60,10 +61,11 @@ def seal_records(key, version, fixed_iv, seq0, n, data, data_off, data_len, ctyp
 
 
 def open_records(key, version, fixed_iv, seq0, n, wire, wire_off, wire_len, data, data_off,
-                 data_len, ctype, status, stream=None):
+                 data_len, ctype, status, stream=None, recv_limit=0):
     """Check, open and de-frame ``n`` wire records; per-record ``status`` codes
-    are in ``STATUS`` (0 = ok)."""
+    are in ``STATUS`` (0 = ok).  ``recv_limit``: the connection's
+    recv_record_limit (0 = 2^14, recordlayer.py:56)."""
     dk = _handle(key)
     r = _records(n, version, fixed_iv, seq0, data, data_off, data_len, ctype, wire, wire_off,
-                 wire_len, status=status)
+                 wire_len, status=status, recv_limit=recv_limit)
     _lib.check(dk._lib.tg_open_records(dk.handle, ctypes.byref(r), _stream(stream)))
