@@ -22,6 +22,7 @@
 // Usable from host code too (the CPU unit test compiles it with g++).
 #pragma once
 #include "aes_bs.h"
+#include "keymath.h"
 
 namespace tg {
 namespace bs8 {
@@ -43,18 +44,9 @@ TG_BS_HD uint32_t rotr_bytes(uint32_t x, int i) {
 
 // Round-key plane (r, i, b) at index (4 r + i) 8 + b: byte c = 0xff iff bit b
 // of byte i of round-key word rk[4 r + c] ^ (r ? 0x63636363 : 0) is set
-// (the S-box constant dropped by the circuit, see aes_bs.h).  rk: LE words of
+// (the S-box constant dropped by the circuit, see aes_bs.h; keymath.h).  rk: LE words of
 // the schedule bytes (GcmKeyDev::rk).  (NR + 1) * 32 words per key.
-TG_BS_HD uint32_t mask_word(const uint32_t* rk, int e) {
-    const int r = e >> 5, i = (e >> 3) & 3, b = e & 7;
-    uint32_t m = 0;
-#pragma unroll
-    for (int c = 0; c < 4; ++c) {
-        const uint32_t w = rk[4 * r + c] ^ (r ? 0x63636363u : 0u);
-        if ((w >> (8 * i + b)) & 1u) m |= 0xffu << (8 * c);
-    }
-    return m;
-}
+TG_BS_HD uint32_t mask_word(const uint32_t* rk, int e) { return bs8_mask_word(rk, e); }
 
 struct KeyPlanes {   // key planes in memory (host: plain reads; device: scalar loads)
     const uint32_t* w;

@@ -8,12 +8,14 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdarg>
+#include <cstddef>
 #include <cstdio>
 #include <cstring>
 #include <string>
 
 #include "aes_bs8.h"
 #include "common.h"
+#include "host.h"
 #include "tlsgpu.h"
 
 namespace {
@@ -38,120 +40,20 @@ int fail(int code, const char* fmt, ...) {
                         __FILE__, __LINE__);                                          \
     } while (0)
 
-// ---- host AES key schedule (FIPS-197 / rijndael.py:922-993) -------------
-struct HostAes {
-    uint8_t sbox[256];
-    HostAes() {
-        uint8_t exp[256], log[256];
-        uint8_t x = 1;
-        for (int i = 0; i < 255; ++i) {
-            exp[i] = x;
-            log[x] = (uint8_t)i;
-            x = (uint8_t)(x ^ xt(x));
-        }
-        for (int v = 0; v < 256; ++v) {
-            uint8_t inv = v ? exp[(255 - log[v]) % 255] : 0;
-            uint8_t s = inv, r = inv;
-            for (int k = 0; k < 4; ++k) {
-                r = (uint8_t)((r << 1) | (r >> 7));
-                s = (uint8_t)(s ^ r);
-            }
-            sbox[v] = (uint8_t)(s ^ 0x63);
-        }
-    }
-    static uint8_t xt(uint8_t a) { return (uint8_t)((a << 1) ^ ((a & 0x80) ? 0x1b : 0)); }
+using tg::host::le32;
 
-    // round-key bytes, 16 * (rounds + 1)
-    int expand(const uint8_t* key, size_t keylen, uint8_t* rk) const {
-        const int nk = (int)keylen / 4, nr = nk + 6, total = 4 * (nr + 1);
-        memcpy(rk, key, keylen);
-        uint8_t rcon = 1;
-        for (int i = nk; i < total; ++i) {
-            uint8_t t[4];
-            memcpy(t, rk + 4 * (i - 1), 4);
-            if (i % nk == 0) {
-                uint8_t t0 = t[0];
-                t[0] = (uint8_t)(sbox[t[1]] ^ rcon);
-                t[1] = sbox[t[2]];
-                t[2] = sbox[t[3]];
-                t[3] = sbox[t0];
-                rcon = xt(rcon);
-            } else if (nk > 6 && i % nk == 4) {
-                for (int k = 0; k < 4; ++k) t[k] = sbox[t[k]];
-            }
-            for (int k = 0; k < 4; ++k) rk[4 * i + k] = (uint8_t)(rk[4 * (i - nk) + k] ^ t[k]);
-        }
-        return nr;
-    }
-
-    void encrypt(const uint8_t* rk, int nr, const uint8_t in[16], uint8_t out[16]) const {
-        uint8_t s[16], t[16];
-        for (int i = 0; i < 16; ++i) s[i] = (uint8_t)(in[i] ^ rk[i]);
-        for (int r = 1; r <= nr; ++r) {
-            for (int c = 0; c < 4; ++c)
-                for (int row = 0; row < 4; ++row) t[4 * c + row] = sbox[s[4 * ((c + row) & 3) + row]];
-            if (r != nr) {
-                for (int c = 0; c < 4; ++c) {
-                    uint8_t* a = t + 4 * c;
-                    uint8_t all = (uint8_t)(a[0] ^ a[1] ^ a[2] ^ a[3]), a0 = a[0];
-                    a[0] = (uint8_t)(a[0] ^ all ^ xt((uint8_t)(a[0] ^ a[1])));
-                    a[1] = (uint8_t)(a[1] ^ all ^ xt((uint8_t)(a[1] ^ a[2])));
-                    a[2] = (uint8_t)(a[2] ^ all ^ xt((uint8_t)(a[2] ^ a[3])));
-                    a[3] = (uint8_t)(a[3] ^ all ^ xt((uint8_t)(a[3] ^ a0)));
-                }
-            }
-            for (int i = 0; i < 16; ++i) s[i] = (uint8_t)(t[i] ^ rk[16 * r + i]);
-        }
-        memcpy(out, s, 16);
-    }
-};
-
-const HostAes& host_aes() {
-    static HostAes a;
-    return a;
-}
-
-uint32_t le32(const uint8_t* p) {
-    return (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16) | ((uint32_t)p[3] << 24);
-}
-
-// GHASH tables in the block byte layout.  A field element is the 16-byte
-// block read as a big-endian integer whose MSB is the x^0 coefficient
-// (aesgcm.py:8-14); multiplying by x is a right shift with the 0xe1 << 120
-// reduction (AESGCM._gcmShift, aesgcm.py:168-178).  V[n] = H * x^n, and
-// M_j[b] = XOR of V[8j + t] over the bits t (MSB first) set in b.
-void build_ghash_tables(const uint8_t h[16], uint4* table) {
-    uint64_t hi = 0, lo = 0;
-    for (int i = 0; i < 8; ++i) hi = (hi << 8) | h[i];
-    for (int i = 8; i < 16; ++i) lo = (lo << 8) | h[i];
-    uint64_t vhi[128], vlo[128];
-    for (int n = 0; n < 128; ++n) {
-        vhi[n] = hi;
-        vlo[n] = lo;
-        const uint64_t carry = lo & 1;
-        lo = (lo >> 1) | (hi << 63);
-        hi >>= 1;
-        if (carry) hi ^= 0xe1ull << 56;
-    }
-    for (int j = 0; j < 16; ++j) {
-        for (int b = 0; b < 256; ++b) {
-            uint64_t zh = 0, zl = 0;
-            for (int t = 0; t < 8; ++t) {
-                if (b & (0x80 >> t)) {
-                    zh ^= vhi[8 * j + t];
-                    zl ^= vlo[8 * j + t];
-                }
-            }
-            uint8_t bytes[16];
-            for (int k = 0; k < 8; ++k) {
-                bytes[k] = (uint8_t)(zh >> (56 - 8 * k));
-                bytes[8 + k] = (uint8_t)(zl >> (56 - 8 * k));
-            }
-            table[j * 256 + b] = make_uint4(le32(bytes), le32(bytes + 4), le32(bytes + 8),
-                                            le32(bytes + 12));
-        }
-    }
-}
+// host.cpp fills the GcmKeyDev image without HIP types: same layout.
+#define TG_SAME_OFFSET(m) \
+    static_assert(offsetof(tg::GcmKeyDev, m) == offsetof(tg::host::GcmKeyImage, m), #m)
+static_assert(sizeof(tg::GcmKeyDev) == sizeof(tg::host::GcmKeyImage), "GcmKeyDev image size");
+TG_SAME_OFFSET(rounds);
+TG_SAME_OFFSET(ghash);
+TG_SAME_OFFSET(bsmask);
+TG_SAME_OFFSET(hpow);
+TG_SAME_OFFSET(ghash64);
+TG_SAME_OFFSET(ghash8);
+TG_SAME_OFFSET(bs8mask);
+#undef TG_SAME_OFFSET
 
 }  // namespace
 
@@ -520,14 +422,9 @@ int tg_key_create(int alg, const uint8_t* keys, size_t keylen, size_t nkeys, tg_
         tg::AesKeyDev* hk = new (std::nothrow) tg::AesKeyDev[nkeys];
         if (!hk) rc = fail(TG_ENOMEM, "out of host memory");
         if (!rc) {
-            const HostAes& aes = host_aes();
             for (size_t i = 0; i < nkeys; ++i) {
-                uint8_t rk[240] = {0};
-                const int nr = aes.expand(keys + keylen * i, keylen, rk);
                 memset(&hk[i], 0, sizeof(hk[i]));
-                for (int w = 0; w < 4 * (nr + 1); ++w) hk[i].rk[w] = le32(rk + 4 * w);
-                k->rounds = nr;
-                memset(rk, 0, sizeof(rk));
+                k->rounds = tg::host::aes_round_words(keys + keylen * i, keylen, hk[i].rk, nullptr);
             }
             const size_t bytes = sizeof(tg::AesKeyDev) * nkeys;
             e = hipMalloc(&k->dev_key, bytes);
@@ -540,25 +437,9 @@ int tg_key_create(int alg, const uint8_t* keys, size_t keylen, size_t nkeys, tg_
         tg::GcmTableKey* hk = new (std::nothrow) tg::GcmTableKey[nkeys];
         if (!hk) rc = fail(TG_ENOMEM, "out of host memory");
         if (!rc) {
-            const HostAes& aes = host_aes();
             for (size_t i = 0; i < nkeys; ++i) {
-                uint8_t rk[240] = {0};
-                const int nr = aes.expand(keys + keylen * i, keylen, rk);
                 memset(&hk[i], 0, sizeof(hk[i]));
-                for (int w = 0; w < 4 * (nr + 1); ++w) hk[i].rk[w] = le32(rk + 4 * w);
-                k->rounds = nr;
-                uint8_t zero[16] = {0}, h[16];
-                aes.encrypt(rk, nr, zero, h);                 // H = E_K(0^128)
-                for (int w = 0; w < 4; ++w) {                 // normal order: per-byte bit reversal
-                    uint32_t v = 0;
-                    for (int bt = 0; bt < 4; ++bt) {
-                        uint8_t x = h[4 * w + bt], r = 0;
-                        for (int t = 0; t < 8; ++t) r = (uint8_t)(r | (((x >> t) & 1) << (7 - t)));
-                        v |= (uint32_t)r << (8 * bt);
-                    }
-                    hk[i].hn[w] = v;
-                }
-                memset(rk, 0, sizeof(rk));
+                k->rounds = tg::host::aes_round_words(keys + keylen * i, keylen, hk[i].rk, hk[i].hn);
             }
             const size_t bytes = sizeof(tg::GcmTableKey) * nkeys;
             e = hipMalloc(&k->dev_key, dev_key_bytes(k));
@@ -573,51 +454,14 @@ int tg_key_create(int alg, const uint8_t* keys, size_t keylen, size_t nkeys, tg_
             delete[] hk;
         }
     } else if (alg == TG_AES_GCM) {
-        tg::GcmKeyDev* hk = new (std::nothrow) tg::GcmKeyDev();
+        auto* hk = new (std::nothrow) tg::host::GcmKeyImage();
         if (!hk) rc = fail(TG_ENOMEM, "out of host memory");
         if (!rc) {
-            uint8_t rk[240];
-            const HostAes& aes = host_aes();
-            const int nr = aes.expand(keys, keylen, rk);
-            for (int w = 0; w < 4 * (nr + 1); ++w) hk->rk[w] = le32(rk + 4 * w);
-            hk->rounds = (uint32_t)nr;
-            k->rounds = nr;
-            uint8_t zero[16] = {0}, h[16];
-            aes.encrypt(rk, nr, zero, h);                     // H = E_K(0^128)
-            build_ghash_tables(h, hk->ghash);
-            for (int e = 0; e < 128 * (nr + 1); ++e) hk->bsmask[e] = tg::bs_mask_word(hk->rk, e);
-            {   // H^1 .. H^kHPow in normal order
-                uint32_t hn[4], p[4];
-                for (int w = 0; w < 4; ++w) hn[w] = tg::gcm_word_to_norm(le32(h + 4 * w));
-                for (int w = 0; w < 4; ++w) p[w] = hn[w];
-                for (int e = 0; e < tg::kHPow; ++e) {
-                    hk->hpow[e] = make_uint4(p[0], p[1], p[2], p[3]);
-                    tg::gf_mul_norm(p, hn, p);
-                }
-            }
-            {   // the tables of H^64 (byte layout of hpow[63])
-                uint8_t h64[16];
-                const uint32_t pw[4] = {hk->hpow[63].x, hk->hpow[63].y, hk->hpow[63].z, hk->hpow[63].w};
-                for (int w = 0; w < 4; ++w) {
-                    const uint32_t v = tg::gcm_word_to_norm(pw[w]);
-                    for (int q = 0; q < 4; ++q) h64[4 * w + q] = (uint8_t)(v >> (8 * q));
-                }
-                build_ghash_tables(h64, hk->ghash64);
-            }
-            {   // the tables of H^8 (gcm_bs8_kernel) and the bitsliced round-key planes
-                uint8_t h8[16];
-                const uint32_t pw[4] = {hk->hpow[7].x, hk->hpow[7].y, hk->hpow[7].z, hk->hpow[7].w};
-                for (int w = 0; w < 4; ++w) {
-                    const uint32_t v = tg::gcm_word_to_norm(pw[w]);
-                    for (int q = 0; q < 4; ++q) h8[4 * w + q] = (uint8_t)(v >> (8 * q));
-                }
-                build_ghash_tables(h8, hk->ghash8);
-                for (int e = 0; e < 32 * (nr + 1); ++e) hk->bs8mask[e] = tg::bs8::mask_word(hk->rk, e);
-            }
+            tg::host::gcm_key_image(keys, keylen, hk);   // key length checked by new_key
+            k->rounds = (int)hk->rounds;
             e = hipMalloc(&k->dev_key, sizeof(tg::GcmKeyDev));
             if (e == hipSuccess) e = hipMemcpy(k->dev_key, hk, sizeof(tg::GcmKeyDev), hipMemcpyHostToDevice);
             if (e != hipSuccess) rc = fail(TG_EHIP, "key upload: %s", hipGetErrorString(e));
-            memset(rk, 0, sizeof(rk));
             memset(hk, 0, sizeof(*hk));
             delete hk;
         }
@@ -790,21 +634,11 @@ int64_t tg_scan_records(const uint8_t* buf, size_t len, uint32_t max_body, uint6
                         uint32_t* rlen, size_t max_n, size_t* consumed) {
     if (!consumed || (len && !buf) || (max_n && (!off || !rlen)))
         return fail(TG_EINVAL, "null argument");
-    size_t pos = 0, k = 0;
-    *consumed = 0;
-    while (k < max_n && len - pos >= 5) {
-        const uint8_t type = buf[pos];
-        if (type < 20 || type > 24) return fail(TG_EHEADER, "record %zu: content type %u", k, type);
-        const uint32_t body = ((uint32_t)buf[pos + 3] << 8) | buf[pos + 4];
-        if (body > max_body) return fail(TG_EOVERFLOW, "record %zu: %u > %u bytes", k, body, max_body);
-        if (len - pos < 5 + (size_t)body) break;   // incomplete: wait for more bytes
-        off[k] = pos;
-        rlen[k] = 5 + body;
-        pos += 5 + body;
-        *consumed = pos;
-        ++k;
-    }
-    return (int64_t)k;
+    tg::host::ScanError err{};
+    const int64_t k = tg::host::scan_records(buf, len, max_body, off, rlen, max_n, consumed, &err);
+    if (k >= 0) return k;
+    if (err.code == 1) return fail(TG_EHEADER, "record %zu: content type %u", err.index, err.value);
+    return fail(TG_EOVERFLOW, "record %zu: %u > %u bytes", err.index, err.value, max_body);
 }
 
 int tg_gather(const uint8_t* src, const uint64_t* src_off, const uint32_t* len, uint8_t* dst,

@@ -4,11 +4,12 @@
 // used by every kernel.  All record data is handled as little-endian 32-bit
 // words of the wire bytes, so a 16-byte block is one uint4 load and no byte
 // swapping happens on the hot path (GHASH tables are built in the same byte
-// layout on the host, see api.cpp).
+// layout on the host, see host.cpp).
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "keymath.h"
 #include "tlsgpu.h"
 
 namespace tg {
@@ -37,69 +38,13 @@ struct GcmKeyDev {
 // first) for e = 1 .. kHPow.
 constexpr int kHPow = 2048;
 
-// a * b in GF(2^128) mod x^128 + x^7 + x^2 + x + 1, normal order, bitwise
-// (key setup only).
-__host__ __device__ inline void gf_mul_norm(const uint32_t a[4], const uint32_t b[4], uint32_t r[4]) {
-    uint32_t z[4] = {0, 0, 0, 0}, v[4] = {b[0], b[1], b[2], b[3]};
-    for (int i = 0; i < 128; ++i) {
-        if ((a[i >> 5] >> (i & 31)) & 1u)
-            for (int q = 0; q < 4; ++q) z[q] ^= v[q];
-        const uint32_t carry = v[3] >> 31;
-        v[3] = (v[3] << 1) | (v[2] >> 31);
-        v[2] = (v[2] << 1) | (v[1] >> 31);
-        v[1] = (v[1] << 1) | (v[0] >> 31);
-        v[0] = (v[0] << 1) ^ (carry ? 0x87u : 0u);
-    }
-    for (int q = 0; q < 4; ++q) r[q] = z[q];
-}
-
-// Normal-order word from a LE word of GCM block bytes: per-byte bit reversal.
-__host__ __device__ inline uint32_t gcm_word_to_norm(uint32_t w) {
-    uint32_t r = 0;
-    for (int k = 0; k < 32; ++k) r |= ((w >> k) & 1u) << ((k & ~7) + 7 - (k & 7));
-    return r;
-}
-
-// Entry e = j * 256 + b of the 8-bit GHASH tables of G (hv: G as LE words of
-// its GCM bytes): b * x^(8j) * G in the same layout (aesgcm.py:8-14 bit order,
-// _mul :86-97 restated bitwise).  Built on the device by keysetup.hip and by
-// the self-test (selftest.hip); api.hip's host builder gives the same tables.
+// Entry e of the 8-bit GHASH tables of G as a uint4 (keymath.h
+// ghash_table_words): built on the device by keysetup.hip and by the
+// self-test (selftest.hip); host.cpp's builder gives the same tables.
 __host__ __device__ inline uint4 ghash_table_entry(const uint32_t hv[4], int e) {
-    const int j = e >> 8, b = e & 255;
-    uint64_t hi = 0, lo = 0;
-#pragma unroll
-    for (int k = 0; k < 8; ++k) hi = (hi << 8) | ((hv[k >> 2] >> (8 * (k & 3))) & 0xff);
-#pragma unroll
-    for (int k = 8; k < 16; ++k) lo = (lo << 8) | ((hv[k >> 2] >> (8 * (k & 3))) & 0xff);
-    uint64_t zh = 0, zl = 0;
-    for (int nsh = 0; nsh < 8 * j + 8; ++nsh) {             // V = H * x^nsh
-        if (nsh >= 8 * j && (b & (0x80 >> (nsh - 8 * j)))) {
-            zh ^= hi;
-            zl ^= lo;
-        }
-        const uint64_t carry = lo & 1;
-        lo = (lo >> 1) | (hi << 63);
-        hi >>= 1;
-        if (carry) hi ^= 0xe1ull << 56;
-    }
     uint32_t w[4];
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-        const uint64_t half = q < 2 ? zh : zl;
-        const int sh = q & 1 ? 24 : 56;
-        uint32_t v = 0;
-#pragma unroll
-        for (int k = 0; k < 4; ++k) v |= (uint32_t)((half >> (sh - 8 * k)) & 0xff) << (8 * k);
-        w[q] = v;
-    }
+    ghash_table_words(hv, e, w);
     return make_uint4(w[0], w[1], w[2], w[3]);
-}
-
-// Entry e of GcmKeyDev::bsmask from the round-key words.
-__host__ __device__ inline uint32_t bs_mask_word(const uint32_t* rk, int e) {
-    const int r = e >> 7, k = (e >> 3) & 15, bit = e & 7;
-    const uint32_t w = rk[4 * r + (k >> 2)] ^ (r ? 0x63636363u : 0u);
-    return ((w >> (8 * (k & 3) + bit)) & 1u) ? 0xffffffffu : 0u;
 }
 
 // One entry of an AES-GCM key table (many sessions in one batch): the round
