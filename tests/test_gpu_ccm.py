@@ -93,7 +93,8 @@ LEN_MIX = [0, 1, 15, 16, 17, 31, 63, 64, 65, 100, 255, 256, 1000, 1024, 1025, 40
 
 @pytest.mark.parametrize("klen,tl", [(16, 16), (32, 16), (16, 8), (32, 8)])
 @pytest.mark.parametrize("align", [16, 1])
-@pytest.mark.parametrize("variant", ["0", "1"])   # counter-window cache / full rounds
+# auto / lane full rounds / wave per record / lane counter-window cache
+@pytest.mark.parametrize("variant", ["0", "1", "2", "3"])
 def test_batch_ragged_vs_oracle(torch, tg, oracle_mod, klen, tl, align, variant):
     from batchpack import HostBatch, run_seal_open
     rng = np.random.default_rng(klen * 11 + tl + align)
@@ -115,8 +116,10 @@ def test_batch_ragged_vs_oracle(torch, tg, oracle_mod, klen, tl, align, variant)
 
 @pytest.mark.parametrize("klen,tl", [(16, 16), (32, 8)])
 @pytest.mark.parametrize("align", [16, 1])
-def test_key_table_vs_oracle(torch, tg, oracle_mod, klen, tl, align):
+@pytest.mark.parametrize("variant", ["2", "3"])   # wave per record / lane per record
+def test_key_table_vs_oracle(torch, tg, oracle_mod, klen, tl, align, variant, monkeypatch):
     from batchpack import HostBatch, run_seal_open
+    monkeypatch.setenv("TLSGPU_CCM_VARIANT", variant)
     rng = np.random.default_rng(3 + klen + tl + align)
     lens = list(rng.integers(0, 4097, 700)) + [0, 1, 15, 16, 17, 16384, 16400]
     hb = HostBatch(lens, payload_seed=4, align=align, aad_mode="tls12", key_count=29, tag=tl)

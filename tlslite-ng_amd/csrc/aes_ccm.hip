@@ -47,6 +47,34 @@ __device__ __forceinline__ uint4 shl_bytes(uint4 v, uint32_t n) {
 
 __device__ __forceinline__ uint4 xor_blk(uint4 a, uint4 b) { return xor4(a, b); }
 
+// CBC-MAC over B_0 and the encoded AAD blocks (aesccm.py:40-67): step(blk)
+// performs x = E(x ^ blk) on the caller's state (x = 0 before B_0).
+// B_0 = flags || nonce || be24(len), then enc(len(aad)) || aad, zero-padded.
+// nv: the nonce as LE words; a1, a2, a3 its words shifted by one byte.
+template <int TAG, class Step>
+__device__ __forceinline__ void ccm_mac_head(Step&& step, uint4 nv, uint32_t a1, uint32_t a2,
+                                             uint32_t a3, uint32_t len, const uint8_t* ad,
+                                             uint32_t alen) {
+    // B_0 (aesccm.py:40-46); the length is numberToByteArray(len, 3)
+    const uint32_t flags = (alen ? 64u : 0u) + 8u * ((TAG - 2) / 2) + 2u;
+    step(make_uint4(flags | (nv.x << 8), a1, a2, a3 | (bswap32(len) & 0xffffff00u)));
+    // enc(len(aad)) || aad, zero-padded (aesccm.py:48-67)
+    if (alen) {
+        const uint32_t np = alen < 0xff00u ? 2u : 6u;
+        const uint4 pre = np == 2 ? make_uint4(((alen >> 8) & 0xffu) | ((alen & 0xffu) << 8), 0, 0, 0)
+                                  : make_uint4(0xfeffu | (((alen >> 24) & 0xffu) << 16) |
+                                                   (((alen >> 16) & 0xffu) << 24),
+                                               ((alen >> 8) & 0xffu) | ((alen & 0xffu) << 8), 0, 0);
+        const uint32_t first = alen < 16 - np ? alen : 16 - np;
+        uint4 blk = shl_bytes(load_partial(ad, first), np);
+        step(make_uint4(blk.x | pre.x, blk.y | pre.y, blk.z, blk.w));
+        for (uint32_t off = first; off < alen; off += 16) {
+            const uint32_t m = alen - off < 16 ? alen - off : 16;
+            step(load_partial(ad + off, m));
+        }
+    }
+}
+
 template <int NR, bool OPEN, int TAG, bool WIN, class RK>
 __device__ __forceinline__ void ccm_record(const tg_batch& b, uint64_t i, uint32_t lane4,
                                            const RK& rk) {
@@ -66,27 +94,9 @@ __device__ __forceinline__ void ccm_record(const tg_batch& b, uint64_t i, uint32
     const CtrCache cc = ctr_cache<NR>(lane4, rk, make_uint4(a0, a1, a2, 0u));
     const uint4 s0 = aes_ctr_w<NR>(lane4, rk, cc, a3);   // E(S_0) masks the tag
 
-    // B_0 (aesccm.py:40-46); the length is numberToByteArray(len, 3)
-    const uint32_t flags = (alen ? 64u : 0u) + 8u * ((TAG - 2) / 2) + 2u;
-    uint4 x = aes_block<NR>(lane4, rk,
-                            make_uint4(flags | (nv.x << 8), a1, a2, a3 | (bswap32(len) & 0xffffff00u)));
-
-    // enc(len(aad)) || aad, zero-padded (aesccm.py:48-67)
-    if (alen) {
-        const uint32_t np = alen < 0xff00u ? 2u : 6u;
-        const uint4 pre = np == 2 ? make_uint4(((alen >> 8) & 0xffu) | ((alen & 0xffu) << 8), 0, 0, 0)
-                                  : make_uint4(0xfeffu | (((alen >> 24) & 0xffu) << 16) |
-                                                   (((alen >> 16) & 0xffu) << 24),
-                                               ((alen >> 8) & 0xffu) | ((alen & 0xffu) << 8), 0, 0);
-        const uint32_t first = alen < 16 - np ? alen : 16 - np;
-        uint4 blk = shl_bytes(load_partial(ad, first), np);
-        blk = make_uint4(blk.x | pre.x, blk.y | pre.y, blk.z, blk.w);
-        x = aes_block<NR>(lane4, rk, xor_blk(x, blk));
-        for (uint32_t off = first; off < alen; off += 16) {
-            const uint32_t m = alen - off < 16 ? alen - off : 16;
-            x = aes_block<NR>(lane4, rk, xor_blk(x, load_partial(ad + off, m)));
-        }
-    }
+    uint4 x = make_uint4(0, 0, 0, 0);
+    ccm_mac_head<TAG>([&](uint4 blk) { x = aes_block<NR>(lane4, rk, xor_blk(x, blk)); }, nv, a1, a2,
+                      a3, len, ad, alen);
 
     // payload: keystream S_1.., CBC-MAC over the plaintext (aesccm.py:68-70)
     const uint32_t nfull = len >> 4;
@@ -157,6 +167,216 @@ __global__ __launch_bounds__(ccm_threads<TABLE>()) void ccm_kernel(const AesKeyD
     ccm_record<NR, OPEN, TAG, WIN>(b, i, lane4, rk);
 }
 
+// ---- one block on the four lanes of a quad (the serial CBC-MAC chain) ----
+// Quad table (wave kernel LDS at 0): row x (256 B apart, 128 B used) holds 4
+// copies each of T0[x], T1[x] = rotl8 T0[x], T2[x] = rotl16 T0[x],
+// T3[x] = rotl24 T0[x] and S[x] << 8k (k = 0..3); lane c reads copy c % 4, so
+// the four lanes of a quad never share a bank.  Table t of row x sits at
+// (x << 8) + 16 t + 4 c: te_addr() builds (x.byteK << 8) | lc with one v_perm
+// and the 16 t rides in the DS offset.
+constexpr uint32_t kQuadRows = 256 * 256;
+template <int T, int K>
+__device__ __forceinline__ uint32_t Q(uint32_t x, uint32_t lc) { return lds_u32(te_addr<K>(x, lc) + 16 * T); }
+
+__device__ __forceinline__ void stage_quad(uint4* q) {
+    for (int e = threadIdx.x; e < 256 * 8; e += blockDim.x) {
+        const uint32_t x = e >> 3, t = e & 7, v = c_te.te0[x];
+        const uint32_t w = t < 4 ? rotl32(v, 8 * t) : ((v >> 8) & 0xffu) << (8 * (t - 4));
+        q[16 * x + t] = make_uint4(w, w, w, w);
+    }
+}
+
+// Lane c holds state column c and the column-c words of the round keys.  It
+// looks up its own column's four bytes -- T0(b0) for column c, T1(b1) for
+// c - 1, T2(b2) for c - 2, T3(b3) for c - 3 (the terms of col()) -- and
+// gathers column c's other three terms from lanes c + 1 .. c + 3 with DPP
+// quad permutes: 4 lookups per round and lane instead of 16 on one lane.
+template <int K>
+__device__ __forceinline__ uint32_t quad_from(uint32_t v) {   // lane c <- lane (c + K) % 4
+    constexpr int ctrl = K == 1 ? 0x39 : (K == 2 ? 0x4e : 0x93);
+    return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, ctrl, 0xf, 0xf, false);
+}
+
+template <int NR>
+__device__ __forceinline__ uint32_t aes_quad(uint32_t lc, const uint32_t (&rkc)[NR + 1], uint32_t x) {
+    uint32_t s = x ^ rkc[0];
+#pragma unroll
+    for (int r = 1; r < NR; ++r) {
+        const uint32_t p0 = Q<0, 0>(s, lc), p1 = Q<1, 1>(s, lc), p2 = Q<2, 2>(s, lc), p3 = Q<3, 3>(s, lc);
+        s = xor3(p0, quad_from<1>(p1), rkc[r]) ^ xor3(quad_from<2>(p2), quad_from<3>(p3), 0u);
+    }
+    const uint32_t p0 = Q<4, 0>(s, lc), p1 = Q<5, 1>(s, lc), p2 = Q<6, 2>(s, lc), p3 = Q<7, 3>(s, lc);
+    return xor3(p0, quad_from<1>(p1), rkc[NR]) ^ xor3(quad_from<2>(p2), quad_from<3>(p3), 0u);
+}
+
+// One full block on one lane from the quad table (the stream wave's counter
+// blocks; up to 16-way bank conflicts, off the critical path).
+template <int NR, class RK>
+__device__ __forceinline__ uint4 aes_block_q(uint32_t lc, const RK& rkp, uint4 in) {
+    const uint4 k0 = rkp.get(0);
+    uint32_t s0 = in.x ^ k0.x, s1 = in.y ^ k0.y, s2 = in.z ^ k0.z, s3 = in.w ^ k0.w;
+#pragma unroll
+    for (int r = 1; r < NR; ++r) {
+        const uint4 k = rkp.get(r);
+        const uint32_t t0 = xor3(Q<0, 0>(s0, lc), Q<1, 1>(s1, lc), k.x) ^ (Q<2, 2>(s2, lc) ^ Q<3, 3>(s3, lc));
+        const uint32_t t1 = xor3(Q<0, 0>(s1, lc), Q<1, 1>(s2, lc), k.y) ^ (Q<2, 2>(s3, lc) ^ Q<3, 3>(s0, lc));
+        const uint32_t t2 = xor3(Q<0, 0>(s2, lc), Q<1, 1>(s3, lc), k.z) ^ (Q<2, 2>(s0, lc) ^ Q<3, 3>(s1, lc));
+        const uint32_t t3 = xor3(Q<0, 0>(s3, lc), Q<1, 1>(s0, lc), k.w) ^ (Q<2, 2>(s1, lc) ^ Q<3, 3>(s2, lc));
+        s0 = t0; s1 = t1; s2 = t2; s3 = t3;
+    }
+    const uint4 k = rkp.get(NR);
+    return make_uint4(xor3(Q<4, 0>(s0, lc), Q<5, 1>(s1, lc), k.x) ^ (Q<6, 2>(s2, lc) ^ Q<7, 3>(s3, lc)),
+                      xor3(Q<4, 0>(s1, lc), Q<5, 1>(s2, lc), k.y) ^ (Q<6, 2>(s3, lc) ^ Q<7, 3>(s0, lc)),
+                      xor3(Q<4, 0>(s2, lc), Q<5, 1>(s3, lc), k.z) ^ (Q<6, 2>(s0, lc) ^ Q<7, 3>(s1, lc)),
+                      xor3(Q<4, 0>(s3, lc), Q<5, 1>(s0, lc), k.w) ^ (Q<6, 2>(s1, lc) ^ Q<7, 3>(s2, lc)));
+}
+
+__device__ __forceinline__ uint32_t word_of(uint4 v, uint32_t c) {
+    return c == 0 ? v.x : (c == 1 ? v.y : (c == 2 ? v.z : v.w));
+}
+
+// ---- wave-per-record kernel (per-record calls and small batches) --------
+// The CBC-MAC chain is serial, the CTR keystream is not.  One record per
+// 128-thread workgroup, two wave roles:
+//   wave 1 (stream wave): for 64-block chunk k, lane t loads payload block
+//     64k + t (one coalesced 1 KiB row per instruction, the next chunk's row
+//     already in flight), XORs it with E(S_{64k+t+1}), stores the output and
+//     stages the MAC input block (plaintext: seal's input, open's output) in
+//     LDS buffer k % 2;
+//   wave 0 (MAC wave): lanes 0-3 run B_0, the AAD blocks and then
+//     x = E(x ^ m) (aes_quad) over the staged blocks of chunk k - 1 while the
+//     stream wave fills chunk k.
+// One workgroup barrier per chunk hands the buffers over, so the record takes
+// about (blocks + 2) serial quad encryptions with the payload's HBM latency
+// and the keystream hidden behind them (the lane kernel pays a dependent HBM
+// load per block).  Both waves read the quad table.
+constexpr int kCcmWaveThreads = 128;
+constexpr uint32_t kCcmStage = kQuadRows;       // 2 x 64 x 16 B staged MAC input
+constexpr uint32_t kCcmMisc = 65536 + 2048;     // E(S_0), open verdict
+constexpr uint32_t kCcmRk = 65536 + 2048 + 32;  // the record's round keys
+constexpr size_t kCcmWaveLds = 65536 + 2048 + 32 + 240;
+
+template <int NR, bool OPEN, int TAG, bool TABLE>
+__global__ __launch_bounds__(kCcmWaveThreads) void ccm_wave_kernel(const AesKeyDev* __restrict__ keys,
+                                                                   tg_batch b) {
+    stage_quad(g_lds_ccm);
+    const uint64_t i = blockIdx.x;                 // the record (workgroup-uniform)
+    const AesKeyDev* kp = TABLE ? keys + b.key_idx[i] : keys;
+    uint32_t* rkw = reinterpret_cast<uint32_t*>(reinterpret_cast<uint8_t*>(g_lds_ccm) + kCcmRk);
+    if (threadIdx.x < 4 * (NR + 1)) rkw[threadIdx.x] = kp->rk[threadIdx.x];
+    const RkLds rk{kCcmRk};                        // round keys read per round from LDS
+    const uint32_t lane = threadIdx.x & 63u, lc = (threadIdx.x & 3u) << 2;
+    const bool mac_wave = threadIdx.x < 64;
+    uint4* stage = reinterpret_cast<uint4*>(reinterpret_cast<uint8_t*>(g_lds_ccm) + kCcmStage);
+    uint4* misc = reinterpret_cast<uint4*>(reinterpret_cast<uint8_t*>(g_lds_ccm) + kCcmMisc);
+
+    const uint8_t* in = rec_in(b, i);
+    uint8_t* out = rec_out(b, i);
+    const uint32_t len = rec_len(b, i);
+    const uint8_t* ad = rec_aad(b, i);
+    const uint32_t alen = rec_aad_len(b, i);
+    const bool aligned = (((uintptr_t)in | (uintptr_t)out) & 15) == 0;
+    const uint4 nv = load_partial(b.nonce + 12 * i, 12);
+    const uint32_t a0 = 2u | (nv.x << 8);
+    const uint32_t a1 = (nv.x >> 24) | (nv.y << 8);
+    const uint32_t a2 = (nv.y >> 24) | (nv.z << 8);
+    const uint32_t a3 = nv.z >> 24;
+    const uint32_t nfull = len >> 4, tail = len & 15, nblk = (len + 15) >> 4;
+    const uint32_t nch = (nblk + 63) >> 6;
+    __syncthreads();                               // Te staged
+
+    uint32_t xc = 0;                               // MAC lanes 0-3: column lane of x
+    uint32_t rkc[NR + 1];
+    if (mac_wave && lane < 4) {
+#pragma unroll
+        for (int r = 0; r <= NR; ++r) rkc[r] = rkw[4 * r + lane];
+    }
+    uint4 nxt = make_uint4(0, 0, 0, 0);
+    if (!mac_wave) {
+        if (lane == 0) misc[0] = aes_block_q<NR>(lc, rk, make_uint4(a0, a1, a2, a3));   // E(S_0) masks the tag
+        if (lane < nfull) nxt = load16(in + 16 * lane, aligned);
+    }
+    for (uint32_t k = 0; k <= nch; ++k) {
+        if (!mac_wave && k < nch) {
+            const uint32_t j = 64 * k + lane;
+            const uint4 d = nxt;
+            if (j + 64 < nfull) nxt = load16(in + 16 * (j + 64), aligned);
+            uint4 m = make_uint4(0, 0, 0, 0);
+            if (j < nblk) {
+                const uint4 ks = aes_block_q<NR>(lc, rk, make_uint4(a0, a1, a2, a3 | (bswap32(j + 1u) & 0xffffff00u)));
+                if (j < nfull) {
+                    const uint4 c = xor4(d, ks);
+                    store16(out + 16 * j, c, aligned);
+                    m = OPEN ? c : d;
+                } else {                           // the partial last block
+                    const uint4 dt = load_partial(in + 16 * j, tail);
+                    const uint4 c = mask_tail(xor4(dt, ks), tail);
+                    store_partial(out + 16 * j, c, tail);
+                    m = OPEN ? c : dt;
+                }
+            }
+            stage[64 * (k & 1) + lane] = m;
+        }
+        if (mac_wave && lane < 4) {
+            if (k == 0) {
+                ccm_mac_head<TAG>([&](uint4 blk) { xc = aes_quad<NR>(lc, rkc, xc ^ word_of(blk, lane)); },
+                                  nv, a1, a2, a3, len, ad, alen);
+            } else {
+                const uint32_t q0 = 64 * (k - 1), cnt = nblk - q0 < 64 ? nblk - q0 : 64;
+                const uint32_t* sb = reinterpret_cast<const uint32_t*>(stage + 64 * ((k - 1) & 1)) + lane;
+                for (uint32_t q = 0; q < cnt; ++q) xc = aes_quad<NR>(lc, rkc, xc ^ sb[4 * q]);
+            }
+        }
+        __syncthreads();
+    }
+    if (mac_wave && lane < 4) {
+        const uint32_t tc = xc ^ reinterpret_cast<const uint32_t*>(misc)[lane];
+        // the auth value (CCM_8 keeps its first 8 bytes), assembled on lane 0
+        const uint4 t = make_uint4(__builtin_amdgcn_readlane(tc, 0), __builtin_amdgcn_readlane(tc, 1),
+                                   __builtin_amdgcn_readlane(tc, 2), __builtin_amdgcn_readlane(tc, 3));
+        if (lane == 0 && !OPEN) {
+            if (TAG == 16) {
+                store16(out + len, t, aligned && tail == 0);
+            } else {
+                store_partial(out + len, t, 8);
+            }
+        } else if (lane == 0) {   // received_mac != computed_mac -> None (aesccm.py:144-146)
+            const uint4 exp = TAG == 16 ? load16(in + len, aligned && tail == 0) : load_partial(in + len, 8);
+            uint32_t diff = (exp.x ^ t.x) | (exp.y ^ t.y);
+            if (TAG == 16) diff |= (exp.z ^ t.z) | (exp.w ^ t.w);
+            if (b.status) b.status[i] = diff == 0;
+            misc[1] = make_uint4(diff, 0, 0, 0);
+        }
+    }
+    if (!OPEN) return;
+    __syncthreads();
+    if (misc[1].x != 0) {                          // zero the released plaintext
+        const uint4 z = make_uint4(0, 0, 0, 0);
+        for (uint32_t q = threadIdx.x; q < nfull; q += kCcmWaveThreads) store16(out + 16 * q, z, aligned);
+        if (tail && threadIdx.x == 0) store_partial(out + 16 * nfull, z, tail);
+    }
+}
+
+template <int NR, bool OPEN, int TAG, bool TABLE>
+int launch_wave(const AesKeyDev* keys, const tg_batch& b, hipStream_t s) {
+    static bool attr_set = false;
+    if (!attr_set) {
+        if (hipFuncSetAttribute((const void*)ccm_wave_kernel<NR, OPEN, TAG, TABLE>,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)kCcmWaveLds) !=
+            hipSuccess)
+            return TG_EHIP;
+        attr_set = true;
+    }
+    hipLaunchKernelGGL((ccm_wave_kernel<NR, OPEN, TAG, TABLE>), dim3((unsigned)b.n),
+                       dim3(kCcmWaveThreads), kCcmWaveLds, s, keys, b);
+    return hipGetLastError() == hipSuccess ? TG_OK : TG_EHIP;
+}
+
+// Up to this many records a batch runs the wave-per-record kernel (two
+// workgroups of 66 KiB LDS per CU: 512 records in flight; at 16 KiB the two
+// kernels meet near 4096 records: profiles/r02/v22_ccm_wave.txt).
+constexpr uint64_t kCcmWaveMaxRecords = 4096;
+
 template <int NR, bool OPEN, int TAG, bool TABLE, bool WIN>
 int launch_w(const AesKeyDev* keys, const tg_batch& b, hipStream_t s) {
     static bool attr_set = false;
@@ -174,10 +394,16 @@ int launch_w(const AesKeyDev* keys, const tg_batch& b, hipStream_t s) {
     return hipGetLastError() == hipSuccess ? TG_OK : TG_EHIP;
 }
 
+// TLSGPU_CCM_VARIANT (read per launch; tests and measurement): 0 = auto (wave
+// per record up to kCcmWaveMaxRecords, else lane per record with the window
+// cache), 1 = lane per record, full rounds, 2 = wave per record, 3 = lane per
+// record with the window cache.
 template <int NR, bool OPEN, int TAG, bool TABLE>
 int launch(const AesKeyDev* keys, const tg_batch& b, hipStream_t s) {
-    const char* e = getenv("TLSGPU_CCM_VARIANT");   // read per launch (tests, measurement)
-    if (e && atoi(e) == 1) return launch_w<NR, OPEN, TAG, TABLE, false>(keys, b, s);
+    const char* e = getenv("TLSGPU_CCM_VARIANT");
+    const int v = e ? atoi(e) : 0;
+    if (v == 1) return launch_w<NR, OPEN, TAG, TABLE, false>(keys, b, s);
+    if (v == 2 || (v == 0 && b.n <= kCcmWaveMaxRecords)) return launch_wave<NR, OPEN, TAG, TABLE>(keys, b, s);
     return launch_w<NR, OPEN, TAG, TABLE, true>(keys, b, s);
 }
 
