@@ -169,3 +169,73 @@ def test_reader_refuses_oversized_inner_plaintext(torch, tg):
     assert [bytes(d) for _, d in ok] == [bytes(detbytes("o%d" % i, 16384)) for i in range(2)]
     with pytest.raises(TLSRecordOverflow):
         r.records()
+
+
+def _mixed_stream(key, iv, n, seed, bad=None):
+    """n TLS 1.3 AES-128-GCM records, every fourth a handshake (22) record,
+    sizes 0..2^14; ``bad``: index of a record with a flipped tag bit."""
+    rng = random.Random(seed)
+    recs, app = [], []
+    for i in range(n):
+        L = rng.choice([0, 1, 17, 300, 4096, 16384, rng.randint(0, 16384)])
+        ct = 22 if i % 4 == 3 else 23
+        pt = detbytes("mix-%d-%d" % (seed, i), L)
+        r = bytearray(orec.seal_record("tls13", "aes128gcm", key, iv, i, ct, pt))
+        if i == bad:
+            r[-1] ^= 1
+        recs.append(bytes(r))
+        app.append(bytes(pt) if ct == 23 else b"")
+    return recs, app
+
+
+@pytest.mark.parametrize("out_kind", ["none", "pageable", "pinned"])
+@pytest.mark.parametrize("batch", [2, 5, 1024])
+def test_read_application_data_pipelined(torch, tg, out_kind, batch):
+    """The bulk path over several pipelined slots: handshake records dropped,
+    application data concatenated in order, whatever the socket read sizes
+    and batch size (recordlayer.py:780-824 per record)."""
+    key, iv = detbytes("bulk-key", 16), detbytes("bulk-iv", 12)
+    recs, app = _mixed_stream(key, iv, 41, batch)
+    wire, want = b"".join(recs), b"".join(app)
+    r = tg.RecordReader(_key(tg, "aesgcm", key), tg.TLS13, iv, batch_records=batch)
+    if out_kind == "pinned":
+        buf = torch.empty(len(want) + 64, dtype=torch.uint8).pin_memory().numpy()
+    else:
+        buf = np.zeros(len(want) + 64, np.uint8)
+    got, pos, rng, fed = bytearray(), 0, random.Random(batch), 0
+    while fed < len(wire):
+        k = rng.choice([3, 700, 20000, 100000, 300000])
+        r.feed(wire[fed:fed + k])
+        fed += k
+        if out_kind == "none":
+            got += r.read_application_data()
+        else:
+            pos += len(r.read_application_data(out=memoryview(buf)[pos:]))
+    if out_kind != "none":
+        got = bytes(buf[:pos])
+    assert bytes(got) == want
+
+
+@pytest.mark.parametrize("batch", [2, 3, 1024])
+def test_read_application_data_errors(torch, tg, batch):
+    """A bad tag in a later pipelined batch: the application data before it is
+    returned, TLSBadRecordMAC on the next call; an oversize header likewise
+    raises TLSRecordOverflow after the records before it."""
+    from tlsgpu.ingest import TLSBadRecordMAC, TLSRecordOverflow
+    key, iv = detbytes("bulk-err", 16), detbytes("bulk-err-iv", 12)
+    recs, app = _mixed_stream(key, iv, 12, 7, bad=9)
+    r = tg.RecordReader(_key(tg, "aesgcm", key), tg.TLS13, iv, batch_records=batch)
+    r.feed(b"".join(recs))
+    assert bytes(r.read_application_data()) == b"".join(app[:9])
+    with pytest.raises(TLSBadRecordMAC):
+        r.read_application_data()
+    recs, app = _mixed_stream(key, iv, 6, 8)
+    r = tg.RecordReader(_key(tg, "aesgcm", key), tg.TLS13, iv, batch_records=batch)
+    r.feed(b"".join(recs) + bytes([23, 3, 3, 0x41, 0x01]) + bytes(0x4101))
+    assert bytes(r.read_application_data()) == b"".join(app)
+    with pytest.raises(TLSRecordOverflow):
+        r.read_application_data()
+    r = tg.RecordReader(_key(tg, "aesgcm", key), tg.TLS13, iv, batch_records=batch)
+    r.feed(bytes([23, 3, 3, 0x41, 0x01]))
+    with pytest.raises(TLSRecordOverflow):
+        r.read_application_data()

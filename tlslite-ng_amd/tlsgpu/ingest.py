@@ -18,10 +18,11 @@ records.py, for the bulk data of one connection direction.
   (tg_open_records) and returned in order as ``(content_type, bytearray)``;
   the first failing record raises the reference's exception.
 
-Each direction keeps ``nslots`` (default 2) slots, each with its own HIP
-stream: while one batch runs host->device copy, kernels and device->host copy,
-the host fills the next slot (writer) or hands the previous batch's records
-to the caller (reader).  Sequence numbers run on from ``seq0`` as in
+Each direction keeps ``nslots`` slots (writer 2, reader 3 by default), each
+with its own HIP stream: while one batch runs host->device copy, kernels and
+device->host copy, the host fills the next slot (writer); the reader's bulk
+path opens batch k+1 while batch k is packed and copied back (both PCIe
+directions busy at once).  Sequence numbers run on from ``seq0`` as in
 ConnectionState.getSeqNumBytes (:251-256).
 """
 import ctypes
@@ -246,7 +247,7 @@ class RecordReader(object):
     """
 
     def __init__(self, key, version, fixed_iv, seq0=0, recv_record_limit=2 ** 14,
-                 batch_records=1024, buffer_bytes=None):
+                 batch_records=1024, buffer_bytes=None, nslots=3):
         import torch
         if version not in (TLS12, TLS13):
             raise ValueError("version must be TLS12 or TLS13")
@@ -275,6 +276,15 @@ class RecordReader(object):
         self.d_src = torch.empty(self.batch, dtype=torch.int64, device="cuda")
         self.d_rl = torch.empty(self.batch, dtype=torch.int32, device="cuda")
         self.h_out = torch.empty(self.batch * self.data_stride, dtype=torch.uint8).pin_memory()
+        # the pipelined bulk path (read_application_data): per-slot gather indices
+        self.rslots = [self.slot] + [_Slot(torch, self.batch, self.data_stride, self.wire_stride,
+                                           self.lead) for _ in range(max(1, nslots) - 1)]
+        for s in self.rslots:
+            s.h_src = torch.empty(self.batch, dtype=torch.int64).pin_memory()
+            s.h_rl = torch.empty(self.batch, dtype=torch.int32).pin_memory()
+            s.h_plen = torch.empty(self.batch, dtype=torch.int32).pin_memory()
+            s.d_src = torch.empty(self.batch, dtype=torch.int64, device="cuda")
+            s.d_rl = torch.empty(self.batch, dtype=torch.int32, device="cuda")
         self.pending_error = None
 
     def feed(self, data):
@@ -288,11 +298,12 @@ class RecordReader(object):
         self.h_buf.numpy()[self.fill:need] = np.frombuffer(mv, np.uint8)
         self.fill = need
 
-    def _scan(self):
+    def _scan(self, start=0):
+        """tg_scan_records over h_buf[start:fill]: (records, bytes, error)."""
         lib = _lib.load()
         consumed = ctypes.c_size_t(0)
-        buf = self.h_buf.numpy()
-        rc = lib.tg_scan_records(buf.ctypes.data, self.fill, self.max_body,
+        buf = self.h_buf.numpy()[start:]
+        rc = lib.tg_scan_records(buf.ctypes.data, self.fill - start, self.max_body,
                                  self.h_off.ctypes.data, self.h_rlen.ctypes.data, self.batch,
                                  ctypes.byref(consumed))
         if rc == _lib.TG_EOVERFLOW:
@@ -319,46 +330,156 @@ class RecordReader(object):
     def read_application_data(self, out=None):
         """The bulk path: the plaintext of every application-data record
         completed so far, concatenated (other content types are dropped, as a
-        caller that reads only application data would).  The records are
-        packed on the device (tg_gather) and copied straight into ``out`` (a
-        writable buffer, filled from offset 0) or a new bytearray; returns
-        that buffer's filled part (bytearray / memoryview).  Raises like
-        records()."""
-        pieces, pos = [], 0
+        caller that reads only application data would), copied into ``out``
+        (a writable buffer, filled from offset 0) or a new bytearray; returns
+        that buffer's filled part (memoryview / bytearray).  Raises like
+        records().
+
+        Pipelined over ``nslots`` slots, each with its own stream: batch k+1's
+        H2D copy and open run while batch k is packed on the device
+        (tg_gather of its application-data plaintexts) and copied back, so the
+        PCIe directions overlap.  When ``out`` is pinned host memory (e.g. the
+        numpy view of a pinned torch tensor) the packed bytes land in it
+        directly and the host never waits for them; otherwise HIP stages the
+        copy (the host waits for it while the next batch is already queued)."""
+        if self.pending_error is not None:
+            e, self.pending_error = self.pending_error, None
+            raise e
+        torch = self.torch
         dst = None if out is None else np.frombuffer(out, np.uint8)
-        for ct, plen in self._batches():
-            n = len(plen)
-            app = ct == APPLICATION_DATA
-            L = plen.astype(np.int64) * app
-            total = int(L.sum())
-            if total == 0:
-                continue
-            s = self.slot
-            h_dst = self.h_src.numpy()
-            h_dst[0] = 0
-            if n > 1:
-                np.cumsum(L[:-1], out=h_dst[1:n])
-            self.h_rl.numpy()[:n] = L.astype(np.int32)
-            with self.torch.cuda.stream(s.stream):
-                self.d_src[:n].copy_(self.h_src[:n], non_blocking=True)
-                self.d_rl[:n].copy_(self.h_rl[:n], non_blocking=True)
-                gather(s.d_data, s.d_data_off, self.d_rl, s.d_pack, self.d_src, n, stream=s.stream)
-            if dst is not None:
-                if pos + total > len(dst):
-                    raise ValueError("output buffer too small")
-                target = dst[pos:pos + total]
-            else:
-                piece = bytearray(total)
-                pieces.append(piece)
-                target = np.frombuffer(piece, np.uint8)
-            _lib.check(_lib.load().tg_memcpy_d2h(target.ctypes.data, s.d_pack.data_ptr(), total,
-                                                 s.stream.cuda_stream))
-            pos += total
+        direct = dst is not None and len(dst) > 0 and torch.from_numpy(dst[:1]).is_pinned()
+        pieces = []
+        self._pos = 0
+        self._got = False
+        self._dead = False
+        meta, done = [], []        # slots opened (metadata pending) / packed (copy pending)
+        free = list(self.rslots)
+        start = 0
+        err = None
+        while not self._dead:
+            n, used, err = self._scan(start)
+            if n:
+                if not free:
+                    if not done:
+                        done.append(self._pack(meta.pop(0), dst, direct, pieces))
+                    free.append(self._finish_read(done.pop(0), dst))
+                s = free.pop(0)
+                self._enqueue_open(s, start, n, used)
+                start += used
+                meta.append(s)
+                if len(meta) > 1:
+                    done.append(self._pack(meta.pop(0), dst, direct, pieces))
+            if err is not None or n < self.batch:
+                break
+        while meta:
+            done.append(self._pack(meta.pop(0), dst, direct, pieces))
+        while done:
+            self._finish_read(done.pop(0), dst)
+        # the unconsumed tail to the front (every copy from h_buf has finished)
+        if self._dead:
+            self.fill = 0
+        else:
+            tail = self.fill - start
+            if tail and start:
+                buf = self.h_buf.numpy()
+                buf[:tail] = buf[start:self.fill].copy()
+            self.fill = tail
+        if err is not None and not self._dead:
+            self.fill = 0
+            self.pending_error = err
+        # an error with no record before it is raised now, else on the next call
+        if self.pending_error is not None and not self._got:
+            e, self.pending_error = self.pending_error, None
+            raise e
         if dst is not None:
-            return memoryview(out)[:pos]
+            return memoryview(out)[:self._pos]
         if len(pieces) == 1:
             return pieces[0]
         return bytearray(b"".join(pieces))
+
+    def _enqueue_open(self, s, start, n, used):
+        """H2D of n scanned records (wire bytes h_buf[start:start+used]),
+        spread into aligned slots, tg_open_records, metadata back; async on
+        the slot's stream.  The slot's sequence number is s.seq."""
+        torch = self.torch
+        src = s.h_src.numpy()
+        src[:n] = self.h_off[:n].astype(np.int64)
+        s.h_rl.numpy()[:n] = self.h_rlen[:n].astype(np.int32)
+        s.n = n
+        s.seq = self.seq
+        self.seq += n
+        with torch.cuda.stream(s.stream):
+            s.d_pack[:used].copy_(self.h_buf[start:start + used], non_blocking=True)
+            s.d_src[:n].copy_(s.h_src[:n], non_blocking=True)
+            s.d_rl[:n].copy_(s.h_rl[:n], non_blocking=True)
+            gather(s.d_pack, s.d_src, s.d_rl, s.d_wire, s.d_wire_off, n, stream=s.stream)
+            open_records(self.key, self.version, self.fixed_iv, s.seq, n, s.d_wire,
+                         s.d_wire_off, s.d_rl, s.d_data, s.d_data_off, s.d_len, s.d_ctype,
+                         s.d_status, stream=s.stream, recv_limit=self.recv_record_limit)
+            s.h_len[:n].copy_(s.d_len[:n], non_blocking=True)
+            s.h_ctype[:n].copy_(s.d_ctype[:n], non_blocking=True)
+            s.h_status[:n].copy_(s.d_status[:n], non_blocking=True)
+            s.event.record(s.stream)
+
+    def _pack(self, s, dst, direct, pieces):
+        """Wait for slot s's metadata; pack its application-data plaintexts
+        (records before the first failing one) on the device and start the
+        copy back to ``dst`` (or a new piece when ``dst`` is None)."""
+        torch = self.torch
+        s.event.synchronize()
+        s.total = 0
+        s.target = None
+        if self._dead:
+            return s
+        n = s.n
+        st = s.h_status.numpy()[:n]
+        bad = np.nonzero(st)[0]
+        k = int(bad[0]) if len(bad) else n
+        if len(bad):
+            cls, msg = _STATUS_EXC.get(int(st[k]), (TLSProtocolException, "record error"))
+            self.pending_error = cls(msg)
+            self._dead = True
+            self.seq = s.seq + k           # later slots were opened past the failure
+        self._got = self._got or k > 0
+        ct = s.h_ctype.numpy()[:k]
+        L = s.h_len.numpy()[:k].astype(np.int64) * (ct == APPLICATION_DATA)
+        total = int(L.sum())
+        s.total = total
+        if total == 0:
+            return s
+        off = s.h_pack.numpy()
+        off[0] = 0
+        if k > 1:
+            np.cumsum(L[:-1], out=off[1:k])
+        s.h_plen.numpy()[:k] = L.astype(np.int32)
+        if dst is not None:
+            if self._pos + total > len(dst):
+                raise ValueError("output buffer too small")
+            s.target = (self._pos, total)
+        else:
+            piece = bytearray(total)
+            pieces.append(piece)
+            s.target = piece
+        with torch.cuda.stream(s.stream):
+            s.d_pack_off[:k].copy_(s.h_pack[:k], non_blocking=True)
+            s.d_wlen[:k].copy_(s.h_plen[:k], non_blocking=True)
+            gather(s.d_data, s.d_data_off, s.d_wlen, s.d_pack, s.d_pack_off, k, stream=s.stream)
+            if isinstance(s.target, bytearray):
+                tgt = np.frombuffer(s.target, np.uint8)
+            else:
+                tgt = dst[self._pos:self._pos + total]
+            # pinned: an async DMA; pageable: HIP's staged copy (blocks the host,
+            # the next batch's open is already queued on its own stream)
+            torch.from_numpy(tgt).copy_(s.d_pack[:total], non_blocking=direct)
+            s.event.record(s.stream)
+        self._pos += total
+        return s
+
+    def _finish_read(self, s, dst):
+        """Wait for slot s's copy back."""
+        s.event.synchronize()
+        s.n = 0
+        return s
 
     def _batches(self):
         """Open the complete records batch by batch; yields (ctype, plen) per
