@@ -10,8 +10,8 @@
 //     call covers the four bytes of a row for all eight blocks), its 0x63
 //     folded into the next round key;
 //   * ShiftRows rotates row i right by i bytes (one v_alignbit per plane);
-//   * MixColumns + AddRoundKey are plane XORs with the round-key planes as
-//     wave-uniform (scalar) operands;
+//   * MixColumns + AddRoundKey are plane XORs with the round-key planes
+//     (scalar operands, or broadcast LDS reads: KeyPlanesLds);
 //   * the last round's ShiftRows is folded into the conversion back to block
 //     words (a byte gather by v_perm plus an 8 x 8 bit transpose per byte).
 // Counter blocks are nonce || be32(c), c = c0 + 64 beta + 8 j for block j of
@@ -48,6 +48,16 @@ TG_BS_HD uint32_t rotr_bytes(uint32_t x, int i) {
 // the schedule bytes (GcmKeyDev::rk).  (NR + 1) * 32 words per key.
 TG_BS_HD uint32_t mask_word(const uint32_t* rk, int e) { return bs8_mask_word(rk, e); }
 
+#if defined(__HIPCC__)
+using Word4 = uint4;
+#else
+struct Word4 {   // the host build (g++, tests/native/bs8_check.cpp) has no HIP vector types
+    uint32_t x, y, z, w;
+};
+#endif
+TG_BS_HD Word4 word4(uint32_t a, uint32_t b, uint32_t c, uint32_t d) { return Word4{a, b, c, d}; }
+
+// Key-plane providers: row4(r, b) = the planes (r, i, b) of rows i = 0..3.
 struct KeyPlanes {   // key planes in memory (host: plain reads; device: scalar loads)
     const uint32_t* w;
     TG_BS_MF uint32_t operator()(int r, int i, int b) const {
@@ -57,7 +67,38 @@ struct KeyPlanes {   // key planes in memory (host: plain reads; device: scalar 
         return w[(4 * r + i) * 8 + b];
 #endif
     }
+    TG_BS_MF Word4 row4(int r, int b) const {
+        return word4((*this)(r, 0, b), (*this)(r, 1, b), (*this)(r, 2, b), (*this)(r, 3, b));
+    }
 };
+
+// The same planes re-laid out in LDS as (8 r + b) * 16 + 4 i: one broadcast
+// ds_read_b128 per (round, bit), so the key XORs take VGPR operands (a
+// v_bitop3 with an SGPR operand issues at half rate on gfx950,
+// profiles/r02/v5_issue_probe2.txt).  stage_lds_planes writes the layout.
+#if defined(__HIPCC__)
+struct KeyPlanesLds {
+    uint32_t base;
+    __device__ __forceinline__ uint4 row4(int r, int b) const {
+#if defined(__HIP_DEVICE_COMPILE__)
+        return *(const __attribute__((address_space(3))) uint4*)(uintptr_t)(base + 16u * (8 * r + b));
+#else
+        return uint4();
+#endif
+    }
+};
+
+// Plane (r, i, b) of the (NR + 1) * 32 in ``src`` (GcmKeyDev::bs8mask order)
+// to LDS ``base`` in KeyPlanesLds order; all threads of the workgroup call it.
+__device__ __forceinline__ void stage_lds_planes(uint32_t base, const uint32_t* src, int nr) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    for (int e = threadIdx.x; e < 32 * (nr + 1); e += blockDim.x) {
+        const int r = e >> 5, i = (e >> 3) & 3, b = e & 7;
+        *(__attribute__((address_space(3))) uint32_t*)(uintptr_t)(base + 16u * (8 * r + b) + 4u * i) = src[e];
+    }
+#endif
+}
+#endif
 
 // The per-record part of the first state (after AddRoundKey 0): plane e =
 // 8 i + b, byte c < 3 = bit e of u[c] (nonce word c ^ rk word c) spread to
@@ -127,9 +168,10 @@ TG_BS_HD void mix_round(uint32_t (*s)[8], const KM& km, int r) {
         for (int i = 0; i < 4; ++i) a[i] = b == 7 ? a7[i] : rotr_bytes(s[i][b], i);
 #pragma unroll
         for (int i = 0; i < 4; ++i) t[i] = b == 7 ? t7[i] : a[i] ^ a[(i + 1) & 3];
+        const Word4 k4 = km.row4(r, b);
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-            const uint32_t k = km(r, i, b);
+            const uint32_t k = i == 0 ? k4.x : (i == 1 ? k4.y : (i == 2 ? k4.z : k4.w));
             const uint32_t tprev = b == 0 ? t7[i] : tp[i];
             if (b == 1 || b == 3 || b == 4)
                 s[i][b] = xor3(xor3(tprev, t7[i], a[(i + 1) & 3]), t[(i + 2) & 3], k);

@@ -40,7 +40,8 @@ constexpr int kBs8Recs = kBs8Threads / 8;               // record slots per work
 constexpr uint32_t kTeBase = 65536;                       // hybrid kernel: Te0/Te2 copies
 constexpr uint32_t kBs8Sbox = 65536;                      // 256-byte S-box
 constexpr uint32_t kBs8Jt = 65536 + 256;                  // gmul_rot lane-offset rows (256 B)
-constexpr uint32_t kBs8RecBase = kBs8Jt + 256;            // 128 B of planes per record slot
+constexpr uint32_t kBs8Keys = kBs8Jt + 256;               // round-key planes (bs8::KeyPlanesLds)
+constexpr uint32_t kBs8RecBase = kBs8Keys + 2048;          // 128 B of planes per record slot
 constexpr size_t kBs8Lds = kBs8RecBase + (kBs8Threads / 64) * 1024;
 
 // No static __shared__ in this file: the GHASH tables sit at LDS address 0
@@ -124,11 +125,11 @@ __device__ __forceinline__ void t_half(uint32_t lane4, const RkLds& rk, const Ct
 // T-table cipher (aes_round.h, Te tables at kTeBase, round keys in SGPRs)
 // instead of the bitsliced one; everything else is shared.  ``recb``: this
 // wave's 1 KiB of LDS for the records' first-state planes.
-template <int NR, bool OPEN, bool TROLE>
+template <int NR, bool OPEN, bool TROLE, class KM>
 __device__ __forceinline__ void octet_job(const GcmKeyDev* __restrict__ key, const tg_batch& b,
                                           const uint32_t* __restrict__ order, uint64_t t0,
                                           uint32_t recw, const RkLds& rkT, uint32_t sbox,
-                                          uint32_t jt) {
+                                          uint32_t jt, const KM& km) {
     const uint32_t* rk = key->rk;
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t l = lane & 7u;
@@ -176,7 +177,6 @@ __device__ __forceinline__ void octet_job(const GcmKeyDev* __restrict__ key, con
         y = xor4(gmul_rot(y, lane & 15u, jt), load_partial(ad + 16 * a, m));
     }
 
-    const bs8::KeyPlanes km{key->bs8mask};
     // the bitsliced cipher leaves out the last round key (folded into the XOR)
     const uint4 rkl = TROLE ? make_uint4(0, 0, 0, 0)
                             : make_uint4(rk[4 * NR] ^ 0x63636363u, rk[4 * NR + 1] ^ 0x63636363u,
@@ -316,10 +316,12 @@ __global__ __launch_bounds__(kBs8Threads, 4) void gcm_bs8_kernel(const GcmKeyDev
                                                                 const uint32_t* __restrict__ order) {
     stage_ghash_rot(g_lds_bs8, key->ghash8, kBs8Jt);
     stage_sbox(kBs8Sbox);
+    bs8::stage_lds_planes(kBs8Keys, key->bs8mask, NR);
     __syncthreads();
     const uint32_t wave = threadIdx.x >> 6;
     octet_job<NR, OPEN, false>(key, b, order, (uint64_t)blockIdx.x * kBs8Recs + 8u * wave,
-                               kBs8RecBase + wave * 1024u, RkLds{0}, kBs8Sbox, kBs8Jt);
+                               kBs8RecBase + wave * 1024u, RkLds{0}, kBs8Sbox, kBs8Jt,
+                               bs8::KeyPlanesLds{kBs8Keys});
 }
 
 // ---- hybrid persistent kernel: T-table waves beside bitsliced waves -------
@@ -334,13 +336,16 @@ constexpr int kHyThreads = 1024;
 constexpr uint32_t kHySbox = 2 * 65536;
 constexpr uint32_t kHyRk = kHySbox + 256;               // 15 round keys (16 B each)
 constexpr uint32_t kHyJt = kHyRk + 256;                 // gmul_rot lane-offset rows
-constexpr uint32_t kHyRecBase = kHyJt + 256;
+constexpr uint32_t kHyKeys = kHyJt + 256;               // round-key planes (bs8::KeyPlanesLds)
+constexpr uint32_t kHyRecBase = kHyKeys + 2048;
 constexpr size_t kHyLds = kHyRecBase + (kHyThreads / 64) * 1024;
 static_assert(kTeBase == 65536, "Te block follows the GHASH tables");
 
 // The batch descriptor is read from memory per job (bp): held in SGPRs
 // across the persistent loop it would crowd out the ciphers' own scalars.
-template <int NR, bool OPEN>
+// LDSKEYS: the bitsliced waves read the round-key planes from LDS (VGPR
+// operands) instead of scalar loads (TLSGPU_HY_KEYS=0 selects it).
+template <int NR, bool OPEN, bool LDSKEYS>
 __global__ __launch_bounds__(kHyThreads) void gcm_hy_kernel(const GcmKeyDev* __restrict__ key,
                                                             const tg_batch* bp,
                                                             const uint32_t* __restrict__ order,
@@ -350,6 +355,7 @@ __global__ __launch_bounds__(kHyThreads) void gcm_hy_kernel(const GcmKeyDev* __r
     stage_te(reinterpret_cast<uint32_t*>(g_lds_bs8) + kTeBase / 4);
     stage_sbox(kHySbox);
     if (threadIdx.x < 4 * (NR + 1)) reinterpret_cast<uint32_t*>(g_lds_bs8)[kHyRk / 4 + threadIdx.x] = key->rk[threadIdx.x];
+    if (LDSKEYS) bs8::stage_lds_planes(kHyKeys, key->bs8mask, NR);
     __syncthreads();
     const uint32_t wave = (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
     const uint64_t njobs = (bp->n + 7) / 8;
@@ -364,7 +370,8 @@ __global__ __launch_bounds__(kHyThreads) void gcm_hy_kernel(const GcmKeyDev* __r
             if (job >= njobs) break;
             asm volatile("" ::: "memory");
             const tg_batch b = *bp;
-            octet_job<NR, OPEN, true>(key, b, order, 8ull * job, recw, rk, kHySbox, kHyJt);
+            octet_job<NR, OPEN, true>(key, b, order, 8ull * job, recw, rk, kHySbox, kHyJt,
+                                      bs8::KeyPlanesLds{kHyKeys});
         }
     } else {
         const RkLds none{0};
@@ -375,7 +382,12 @@ __global__ __launch_bounds__(kHyThreads) void gcm_hy_kernel(const GcmKeyDev* __r
             if (job >= njobs) break;
             asm volatile("" ::: "memory");
             const tg_batch b = *bp;
-            octet_job<NR, OPEN, false>(key, b, order, 8ull * job, recw, none, kHySbox, kHyJt);
+            if (LDSKEYS)
+                octet_job<NR, OPEN, false>(key, b, order, 8ull * job, recw, none, kHySbox, kHyJt,
+                                           bs8::KeyPlanesLds{kHyKeys});
+            else
+                octet_job<NR, OPEN, false>(key, b, order, 8ull * job, recw, none, kHySbox, kHyJt,
+                                           bs8::KeyPlanes{key->bs8mask});
         }
     }
 }
@@ -403,22 +415,16 @@ int launch_bs8(const GcmKeyDev* key, const tg_batch& b, hipStream_t s, const uin
     return hipGetLastError() == hipSuccess ? TG_OK : TG_EHIP;
 }
 
-// TLSGPU_HY_T (T-table waves per 16, default 8) and TLSGPU_HY_PRIO (default 1)
-// are read per launch (measurement).
-template <int NR, bool OPEN>
-int launch_hy(const GcmKeyDev* key, const tg_batch& b, hipStream_t s, const uint32_t* order) {
+template <int NR, bool OPEN, bool LDSKEYS>
+int launch_hy_k(const GcmKeyDev* key, const tg_batch& b, hipStream_t s, const uint32_t* order,
+                uint32_t nt, uint32_t prio) {
     static bool attr_set = false;
     if (!attr_set) {
-        if (hipFuncSetAttribute((const void*)gcm_hy_kernel<NR, OPEN>,
+        if (hipFuncSetAttribute((const void*)gcm_hy_kernel<NR, OPEN, LDSKEYS>,
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)kHyLds) != hipSuccess)
             return TG_EHIP;
         attr_set = true;
     }
-    if ((b.n + 7) / 8 > 0xffffffffull) return TG_EINVAL;
-    const char* et = getenv("TLSGPU_HY_T");
-    const char* ep = getenv("TLSGPU_HY_PRIO");
-    const uint32_t nt = et ? (uint32_t)atoi(et) : 8u;
-    const uint32_t prio = ep ? (uint32_t)atoi(ep) : 1u;
     // job counter + batch copy: stream-ordered scratch, so concurrent batches
     // never share them
     uint8_t* scratch = nullptr;
@@ -428,12 +434,28 @@ int launch_hy(const GcmKeyDev* key, const tg_batch& b, hipStream_t s, const uint
     hipLaunchKernelGGL(hy_setup_kernel, dim3(1), dim3(1), 0, s, b, queue, bcopy);
     bool ok = hipGetLastError() == hipSuccess;
     if (ok) {
-        hipLaunchKernelGGL((gcm_hy_kernel<NR, OPEN>), dim3((unsigned)device_cus()), dim3(kHyThreads), kHyLds,
-                           s, key, (const tg_batch*)bcopy, order, queue, nt, prio);
+        hipLaunchKernelGGL((gcm_hy_kernel<NR, OPEN, LDSKEYS>), dim3((unsigned)device_cus()), dim3(kHyThreads),
+                           kHyLds, s, key, (const tg_batch*)bcopy, order, queue, nt, prio);
         ok = hipGetLastError() == hipSuccess;
     }
     if (hipFreeAsync(scratch, s) != hipSuccess) return TG_EHIP;
     return ok ? TG_OK : TG_EHIP;
+}
+
+// TLSGPU_HY_T (T-table waves per 16, default 8), TLSGPU_HY_PRIO (default 1)
+// and TLSGPU_HY_KEYS (1: key planes by scalar loads, default; 0: from LDS,
+// 2 % slower in the hybrid: the T-table waves own the LDS,
+// profiles/r02/v25_hy_keys.txt) are read per launch (measurement).
+template <int NR, bool OPEN>
+int launch_hy(const GcmKeyDev* key, const tg_batch& b, hipStream_t s, const uint32_t* order) {
+    if ((b.n + 7) / 8 > 0xffffffffull) return TG_EINVAL;
+    const char* et = getenv("TLSGPU_HY_T");
+    const char* ep = getenv("TLSGPU_HY_PRIO");
+    const char* ek = getenv("TLSGPU_HY_KEYS");
+    const uint32_t nt = et ? (uint32_t)atoi(et) : 8u;
+    const uint32_t prio = ep ? (uint32_t)atoi(ep) : 1u;
+    if (ek && atoi(ek) == 0) return launch_hy_k<NR, OPEN, true>(key, b, s, order, nt, prio);
+    return launch_hy_k<NR, OPEN, false>(key, b, s, order, nt, prio);
 }
 
 }  // namespace
