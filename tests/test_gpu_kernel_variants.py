@@ -86,6 +86,7 @@ def test_auto_wave_per_record_batch(torch, tg, oracle_mod, alg, klen):
 
 
 @pytest.mark.parametrize("alg,klen,keys,gcmv", [("aesgcm", 16, 1, "7"), ("aesgcm", 16, 1, "14"),
+                                               ("aesgcm", 16, 1, "15"), ("aesgcm", 32, 1, "15"),
                                                ("chacha", 32, 1, None), ("aesgcm", 32, 29, None),
                                                ("chacha", 32, 29, None)])
 @pytest.mark.parametrize("align", [16, 1])
@@ -110,6 +111,18 @@ def test_planned_mixed_batch(torch, tg, oracle_mod, alg, klen, keys, gcmv, align
         env = ("TLSGPU_GCM_TABLE_VARIANT", "0")   # AES: the lane kernel
     with _with_env(*env):
         run_seal_open(torch, tg, oracle_mod, hb, alg, karr, obj, tamper=(7, 2500, 5019))
+
+
+def test_auto_mixed_batch_hybrid(torch, tg, oracle_mod):
+    """A mixed-length single-key AES-GCM batch above kWaveMaxRecords runs the
+    planner and the hybrid octet kernel by default (aes_gcm.hip)."""
+    from batchpack import HostBatch, run_seal_open
+    rng = np.random.default_rng(77)
+    lens = list(rng.integers(0, 3000, 26000)) + [16384, 16400, 0, 1] * 5
+    hb = HostBatch(lens, payload_seed=11, align=16, aad_mode="tls13")
+    key = rng.bytes(16)
+    run_seal_open(torch, tg, oracle_mod, hb, "aesgcm", np.frombuffer(key, np.uint8),
+                  tg.HipAESGCM(bytearray(key)), tamper=(3, 13000, 26019))
 
 
 @pytest.mark.parametrize("alg,klen", [("aesgcm", 16), ("chacha", 32)])

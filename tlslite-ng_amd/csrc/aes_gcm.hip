@@ -1055,13 +1055,13 @@ int launch_v(const GcmKeyDev* key, const tg_batch& b, hipStream_t s, const uint3
 //   15         the hybrid octet kernel (T-table + bitsliced waves), the default
 //              above kWaveMaxRecords (TLSGPU_HY_T / TLSGPU_HY_PRIO tune it);
 //   16         the T-table lane-per-record kernel that was the default before.
-// Up to this many records a batch runs one record per wavefront: a lane per
-// record leaves most of the GPU idle while one lane walks a whole record
-// until the batch fills every lane slot of the chip; at 16 KiB the two
-// kernels meet at 196 608 records since the lane kernel's counter-window
-// cache (profiles/r01/v31_smallbatch.txt; 2^18 before it, v21_smallbatch.txt),
-// and the wave kernel needs no length planning for mixed batches.
-constexpr uint64_t kWaveMaxRecords = 196608;
+// Up to this many records a batch runs one record per wavefront; above it the
+// hybrid octet kernel, whose floor is one octet job (8 records on one wave,
+// ~0.42 ms at 16 KiB): at 16 KiB the two meet between 16 384 and 32 768
+// records (profiles/r02/v28_wave_vs_hybrid.txt; against the T-table lane
+// kernel it was 196 608, profiles/r01/v31_smallbatch.txt), and the wave
+// kernel needs no length planning for mixed batches.
+constexpr uint64_t kWaveMaxRecords = 24576;
 
 int variant() {
     const char* e = getenv("TLSGPU_GCM_VARIANT");
