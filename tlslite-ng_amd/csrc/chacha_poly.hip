@@ -96,75 +96,122 @@ __device__ __forceinline__ uint32_t wave_min(uint32_t v) {
     return v;
 }
 
-// Per-wave LDS: a 64-record x 64-byte tile (row r = the record of lane r, its
-// four 16-byte chunks XOR-swizzled by (r >> 2) & 3 so that both the row-wise
-// and the coalesced accesses are bank-conflict-free) and the records' in/out
-// base pointers.
+// Per-wave LDS: a 64-record x 128-byte tile -- row r = the record of lane r,
+// holding one aligned pair of 64-byte blocks (one 128-byte HBM line) -- and
+// the records' in/out base pointers.  The row's eight 16-byte chunks are
+// XOR-swizzled by (r >> 1) & 7, so both the row-wise accesses (16 lanes, 16
+// rows) and the coalesced ones (8 lanes per row) are bank-conflict-free.
 struct WaveTile {
-    uint4 row[64][4];
+    uint4 row[64][8];
     uint4 ptr[64];  // {in lo, in hi, out lo, out hi}
 };
 constexpr int kWavesPerGroup = kChachaThreads / 64;
 
-__device__ __forceinline__ uint32_t swz(uint32_t r, uint32_t c) { return c ^ ((r >> 2) & 3); }
+__device__ __forceinline__ uint32_t swz(uint32_t r, uint32_t c) { return c ^ ((r >> 1) & 7u); }
+
+// 16-byte global accesses through pointers read back from LDS: without the
+// address space the compiler emits FLAT instructions, which also count on
+// lgkmcnt, so every LDS wait would wait for the HBM load too.
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ uint4 gload16(const uint8_t* p) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    const u32x4 v = *(const __attribute__((address_space(1))) u32x4*)p;
+    return make_uint4(v.x, v.y, v.z, v.w);
+#else
+    return uint4();
+#endif
+}
+__device__ __forceinline__ void gstore16(uint8_t* p, uint4 v) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    *(__attribute__((address_space(1))) u32x4*)p = u32x4{v.x, v.y, v.z, v.w};
+#endif
+}
 
 // Blocks [0, jmin) of all 64 records of a wave (every record has >= jmin full
-// blocks and 16-byte aligned buffers).  HBM traffic is coalesced through the
-// tile: for load/store instruction q, lane L moves chunk L%4 of record
-// 16q + L/4, i.e. 16 records x 64 contiguous bytes per instruction, instead of
-// 64 scattered 16-byte pieces.  The keystream/Poly1305 pipeline is the same as
-// full_blocks().
+// blocks and 16-byte aligned buffers).  HBM traffic goes through the tile in
+// whole 128-byte lines: coalesced instruction q of row group g moves chunk
+// lane % 8 of the block pair of record 32 g + 8 q + lane / 8, i.e. 8 records
+// x 128 contiguous bytes (a half-line per record and instruction read the
+// other half after it had left L2: 1.3x the algorithmic HBM bytes,
+// profiles/r02/v27/traffic.json).  Rows 0-31 (group A) take the pairs
+// (p, p + 1), p even, at iteration p; rows 32-63 (group B) run one block
+// behind (block b at iteration b + 1), so each iteration moves one group's
+// pair in and the other group's finished pair out -- 4 load and 4 store
+// instructions, as with 64-byte rows.  The keystream/Poly1305 pipeline is
+// the same as full_blocks(); a lane's next keystream block is b + 1.
 template <bool OPEN>
 __device__ __forceinline__ void tiled_blocks(WaveTile& t, uint32_t lane, uint32_t nvalid,
                                              const uint32_t (&k)[8], uint4 nv, uint32_t jmin,
                                              Poly& p, uint32_t (&ks)[16]) {
-    const uint32_t cq = lane & 3;
-    uint4 R[4];
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-        const uint32_t r = 16 * q + (lane >> 2);
-        const uint4 pr = t.ptr[r];
-        const uint8_t* src = reinterpret_cast<const uint8_t*>(((uint64_t)pr.y << 32) | pr.x);
-        R[q] = r < nvalid ? *reinterpret_cast<const uint4*>(src + 16 * cq) : make_uint4(0, 0, 0, 0);
-    }
-    for (uint32_t j = 0; j < jmin; ++j) {
+    const uint32_t grp = lane >> 5, cq = lane & 7u, rq = lane >> 3;
+    // the coalesced ops of group g's pair starting at block p0 (even)
+    auto load_pair = [&](uint32_t g, uint32_t p0, uint4 (&R)[4]) {
+        const uint32_t blk = p0 + (cq >> 2);
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
-            const uint32_t r = 16 * q + (lane >> 2);
-            t.row[r][swz(r, cq)] = R[q];
-        }
-        __builtin_amdgcn_wave_barrier();
-        const uint32_t jn = j + 1 < jmin ? j + 1 : j;
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            const uint32_t r = 16 * q + (lane >> 2);
+            const uint32_t r = 32 * g + 8 * q + rq;
             const uint4 pr = t.ptr[r];
             const uint8_t* src = reinterpret_cast<const uint8_t*>(((uint64_t)pr.y << 32) | pr.x);
-            if (r < nvalid) R[q] = *reinterpret_cast<const uint4*>(src + 64 * jn + 16 * cq);
+            if (r < nvalid && blk < jmin) R[q] = gload16(src + 64 * p0 + 16 * cq);
         }
-        uint4 m[4];
-#pragma unroll
-        for (int c = 0; c < 4; ++c) {
-            const uint4 d = t.row[lane][swz(lane, c)];
-            const uint4 ct = make_uint4(d.x ^ ks[4 * c], d.y ^ ks[4 * c + 1], d.z ^ ks[4 * c + 2],
-                                        d.w ^ ks[4 * c + 3]);
-            t.row[lane][swz(lane, c)] = ct;
-            m[c] = OPEN ? d : ct;
-        }
-        __builtin_amdgcn_wave_barrier();
+    };
+    auto put_pair = [&](uint32_t g, const uint4 (&R)[4]) {
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
-            const uint32_t r = 16 * q + (lane >> 2);
+            const uint32_t r = 32 * g + 8 * q + rq;
+            t.row[r][swz(r, cq)] = R[q];
+        }
+    };
+    auto store_pair = [&](uint32_t g, uint32_t p0) {
+        const uint32_t blk = p0 + (cq >> 2);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const uint32_t r = 32 * g + 8 * q + rq;
             const uint4 v = t.row[r][swz(r, cq)];
             const uint4 pr = t.ptr[r];
             uint8_t* dst = reinterpret_cast<uint8_t*>(((uint64_t)pr.w << 32) | pr.z);
-            if (r < nvalid) *reinterpret_cast<uint4*>(dst + 64 * j + 16 * cq) = v;
+            if (r < nvalid && blk < jmin) gstore16(dst + 64 * p0 + 16 * cq, v);
+        }
+    };
+    uint4 R[4];
+    load_pair(0, 0, R);
+    for (uint32_t i = 0; i <= jmin; ++i) {
+        // group A's pair (i, i + 1) at even i, group B's (i - 1, i) at odd i
+        const uint32_t g = i & 1u, p0 = i - g;
+        if (p0 < jmin) put_pair(g, R);
+        __builtin_amdgcn_wave_barrier();
+        if (i + 1 - ((i + 1) & 1u) < jmin) load_pair((i + 1) & 1u, i + 1 - ((i + 1) & 1u), R);
+        const uint32_t b = i - grp;                 // this lane's block
+        const bool act = i >= grp && b < jmin;
+        uint4 m[4];
+        if (act) {
+            const uint32_t h = 4 * (b & 1u);
+#pragma unroll
+            for (int c = 0; c < 4; ++c) {
+                const uint4 d = t.row[lane][swz(lane, h + c)];
+                const uint4 ct = make_uint4(d.x ^ ks[4 * c], d.y ^ ks[4 * c + 1], d.z ^ ks[4 * c + 2],
+                                            d.w ^ ks[4 * c + 3]);
+                t.row[lane][swz(lane, h + c)] = ct;
+                m[c] = OPEN ? d : ct;
+            }
         }
         __builtin_amdgcn_wave_barrier();
-        chacha_block(k, j + 2, nv.x, nv.y, nv.z, ks);
+        // the pair finished now: group A's (i - 1, i) at odd i, group B's
+        // (i - 2, i - 1) at even i >= 2
+        if (i & 1u) {
+            store_pair(0, i - 1);
+        } else if (i >= 2) {
+            store_pair(1, i - 2);
+        }
+        __builtin_amdgcn_wave_barrier();
+        if (act) {
+            chacha_block(k, b + 2, nv.x, nv.y, nv.z, ks);
 #pragma unroll
-        for (int c = 0; c < 4; ++c) poly_block(p, m[c]);
+            for (int c = 0; c < 4; ++c) poly_block(p, m[c]);
+        }
     }
+    // group B's last pair when jmin is odd (its block jmin - 1 ran at iteration jmin)
+    if (jmin & 1u) store_pair(1, jmin - 1);
 }
 
 template <bool OPEN, bool MULTIKEY, int MINW>
@@ -390,8 +437,9 @@ int launch_w(const ChachaKeyDev* keys, const tg_batch& b, hipStream_t s, const u
 
 // Variants (TLSGPU_CHACHA_VARIANT, read per launch; tests and measurement):
 // 0 = auto (wave per record up to kWaveMaxRecords records, else lane per
-// record), 1 / 2 = lane per record asking for 5 / 6 waves per SIMD,
-// 3 = wave per record, 4 = lane per record.
+// record at 4 waves per SIMD, i.e. <= 128 VGPRs), 1 / 2 = lane per record
+// asking for 5 / 6 waves per SIMD, 3 = wave per record, 4 = lane per record,
+// 5 = lane per record without an occupancy request.
 int chacha_variant() {
     const char* e = getenv("TLSGPU_CHACHA_VARIANT");
     return e ? atoi(e) : 0;
@@ -425,7 +473,8 @@ int launch(const ChachaKeyDev* keys, const tg_batch& b, hipStream_t s, const uin
     switch (v) {
         case 1: return launch_w<OPEN, MULTIKEY, 5>(keys, b, s, order);
         case 2: return launch_w<OPEN, MULTIKEY, 6>(keys, b, s, order);
-        default: return launch_w<OPEN, MULTIKEY, 1>(keys, b, s, order);
+        case 5: return launch_w<OPEN, MULTIKEY, 1>(keys, b, s, order);
+        default: return launch_w<OPEN, MULTIKEY, 4>(keys, b, s, order);
     }
 }
 

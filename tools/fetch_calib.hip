@@ -7,8 +7,9 @@
 //   hipcc -O3 --offload-arch=gfx950 -o fetch_calib tools/fetch_calib.hip
 // Shapes (per wave instruction, 16 B per lane):
 //   coalesced  1 KiB contiguous
-//   octet      8 records x 128 B (aes_gcm_bs8.hip: lane 8q + l of record q)
-//   tile64     16 records x 64 B (chacha_poly.hip tiled_blocks)
+//   octet      8 records x 128 B (aes_gcm_bs8.hip: lane 8q + l of record q;
+//              chacha_poly.hip tiled_blocks since round 2)
+//   tile64     16 records x 64 B (chacha_poly.hip tiled_blocks in round 1)
 //   lane       64 records x 16 B (lane per record, no tile)
 #include <hip/hip_runtime.h>
 #include <stdint.h>

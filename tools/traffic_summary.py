@@ -11,7 +11,8 @@ bytes / counter bytes; a kernel's traffic is its raw counters times the
 factors of its shape:
 
   aes128gcm_*        gcm_hy_kernel (octet: 8 records x 128 B per instruction)
-  chacha20-poly1305_* chacha_kernel (tile64: 16 records x 64 B per instruction)
+  chacha20-poly1305_* chacha_kernel (octet too since round 2's line-pair tile;
+                      it was tile64, 16 records x 64 B per instruction)
 
 The headline working set (48 GiB) is far past the 256 MiB Infinity Cache, so
 cache hits in the counters are negligible.
@@ -30,8 +31,8 @@ CAL_BYTES = 16384 * (1 << 18)
 CAL = {"k_coalesced": "coalesced", "k_octet": "octet", "k_tile64": "tile64", "k_lane": "lane"}
 KERNELS = [(r"gcm_hy_kernel<10, false", "aes128gcm_seal", "octet"),
            (r"gcm_hy_kernel<10, true", "aes128gcm_open", "octet"),
-           (r"chacha_kernel<false", "chacha20-poly1305_seal", "tile64"),
-           (r"chacha_kernel<true", "chacha20-poly1305_open", "tile64")]
+           (r"chacha_kernel<false", "chacha20-poly1305_seal", "octet"),
+           (r"chacha_kernel<true", "chacha20-poly1305_open", "octet")]
 
 
 def collect(d, pattern):
