@@ -190,13 +190,13 @@ __device__ __forceinline__ void octet_job(const GcmKeyDev* __restrict__ key, con
                 uint4 d[N];
 #pragma unroll
                 for (int q = 0; q < N; ++q)
-                    d[q] = *reinterpret_cast<const uint4*>(in + 16u * (blk0 + 8u * (j0 + q)));
+                    d[q] = gload16(in + 16u * (blk0 + 8u * (j0 + q)));
 #pragma unroll
                 for (int q = 0; q < N; ++q) {
                     const uint4 k = ks[q];
                     const uint4 c = make_uint4(xor3(d[q].x, k.x, rkl.x), xor3(d[q].y, k.y, rkl.y),
                                                xor3(d[q].z, k.z, rkl.z), xor3(d[q].w, k.w, rkl.w));
-                    *reinterpret_cast<uint4*>(out + 16u * (blk0 + 8u * (j0 + q))) = c;
+                    gstore16(out + 16u * (blk0 + 8u * (j0 + q)), c);
                     if (!OPEN) d[q] = c;
                 }
 #pragma unroll

@@ -109,23 +109,6 @@ constexpr int kWavesPerGroup = kChachaThreads / 64;
 
 __device__ __forceinline__ uint32_t swz(uint32_t r, uint32_t c) { return c ^ ((r >> 1) & 7u); }
 
-// 16-byte global accesses through pointers read back from LDS: without the
-// address space the compiler emits FLAT instructions, which also count on
-// lgkmcnt, so every LDS wait would wait for the HBM load too.
-typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-__device__ __forceinline__ uint4 gload16(const uint8_t* p) {
-#if defined(__HIP_DEVICE_COMPILE__)
-    const u32x4 v = *(const __attribute__((address_space(1))) u32x4*)p;
-    return make_uint4(v.x, v.y, v.z, v.w);
-#else
-    return uint4();
-#endif
-}
-__device__ __forceinline__ void gstore16(uint8_t* p, uint4 v) {
-#if defined(__HIP_DEVICE_COMPILE__)
-    *(__attribute__((address_space(1))) u32x4*)p = u32x4{v.x, v.y, v.z, v.w};
-#endif
-}
 
 // Blocks [0, jmin) of all 64 records of a wave (every record has >= jmin full
 // blocks and 16-byte aligned buffers).  HBM traffic goes through the tile in

@@ -64,6 +64,25 @@ struct ChachaKeyDev {
     uint32_t k[8];         // key as LE words (chacha.py:101, _bytearray_to_words)
 };
 
+// 16-byte global accesses through pointers the compiler cannot place (read
+// back from LDS or from a descriptor in memory): without the address space it
+// emits FLAT instructions, which also count on lgkmcnt, so every LDS wait
+// would wait for the HBM access too.
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ uint4 gload16(const uint8_t* p) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    const u32x4 v = *(const __attribute__((address_space(1))) u32x4*)p;
+    return make_uint4(v.x, v.y, v.z, v.w);
+#else
+    return uint4();
+#endif
+}
+__device__ __forceinline__ void gstore16(uint8_t* p, uint4 v) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    *(__attribute__((address_space(1))) u32x4*)p = u32x4{v.x, v.y, v.z, v.w};
+#endif
+}
+
 __device__ __forceinline__ uint4 xor4(uint4 a, uint4 b) {
     return make_uint4(a.x ^ b.x, a.y ^ b.y, a.z ^ b.z, a.w ^ b.w);
 }
@@ -92,32 +111,46 @@ __device__ __forceinline__ uint32_t rec_aad_len(const tg_batch& b, uint64_t i) {
     return b.aad_len ? b.aad_len[i] : b.fixed_aad_len;
 }
 
+// Record memory is global.  The record pointers come out of the batch
+// descriptor, so the compiler cannot place them and would emit FLAT accesses
+// (which also count on lgkmcnt: an LDS wait then waits for HBM too); these
+// helpers address global memory explicitly.
+#if defined(__HIP_DEVICE_COMPILE__)
+typedef const __attribute__((address_space(1))) uint8_t* gptr_c;
+typedef __attribute__((address_space(1))) uint8_t* gptr;
+#else
+typedef const uint8_t* gptr_c;
+typedef uint8_t* gptr;
+#endif
+
 // n (<= 16) bytes from p, zero-padded, as 4 LE words.  Fully unrolled with
 // compile-time word indices so nothing is placed in scratch.
 __device__ __forceinline__ uint4 load_partial(const uint8_t* p, uint32_t n) {
+    const gptr_c g = (gptr_c)p;
     uint32_t w[4] = {0, 0, 0, 0};
 #pragma unroll
     for (uint32_t k = 0; k < 16; ++k)
-        if (k < n) w[k >> 2] |= (uint32_t)p[k] << (8 * (k & 3));
+        if (k < n) w[k >> 2] |= (uint32_t)g[k] << (8 * (k & 3));
     return make_uint4(w[0], w[1], w[2], w[3]);
 }
 
 __device__ __forceinline__ void store_partial(uint8_t* p, uint4 v, uint32_t n) {
+    const gptr g = (gptr)p;
     const uint32_t w[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
     for (uint32_t k = 0; k < 16; ++k)
-        if (k < n) p[k] = (uint8_t)(w[k >> 2] >> (8 * (k & 3)));
+        if (k < n) g[k] = (uint8_t)(w[k >> 2] >> (8 * (k & 3)));
 }
 
 // Full 16-byte block; the vector form when the record is 16-byte aligned.
 __device__ __forceinline__ uint4 load16(const uint8_t* p, bool aligned) {
-    if (aligned) return *reinterpret_cast<const uint4*>(p);
+    if (aligned) return gload16(p);
     return load_partial(p, 16);
 }
 
 __device__ __forceinline__ void store16(uint8_t* p, uint4 v, bool aligned) {
     if (aligned) {
-        *reinterpret_cast<uint4*>(p) = v;
+        gstore16(p, v);
     } else {
         store_partial(p, v, 16);
     }
