@@ -135,7 +135,7 @@ __device__ __forceinline__ void octet_job(const GcmKeyDev* __restrict__ key, con
     const uint32_t l = lane & 7u;
     const uint64_t t = t0 + (lane >> 3);
     const bool valid = t < b.n;
-    const uint64_t i = valid ? (order ? order[t] : t) : 0;
+    const uint64_t i = valid ? (order ? gld(order, t) : t) : 0;
     uint32_t len = 0, alen = 0;
     const uint8_t* in = nullptr;
     uint8_t* out = nullptr;
@@ -290,7 +290,7 @@ __device__ __forceinline__ void octet_job(const GcmKeyDev* __restrict__ key, con
     if (valid && l == 0) {
         const uint4 exp = load16(in + len, tag_aligned);
         diff = (exp.x ^ tag.x) | (exp.y ^ tag.y) | (exp.z ^ tag.z) | (exp.w ^ tag.w);
-        if (b.status) b.status[i] = diff == 0;
+        if (b.status) gst(b.status, i, (uint8_t)(diff == 0));
     }
     diff = (uint32_t)__shfl((int)diff, (int)(lane & 56u), 64);
     if (valid && diff) {   // a rejected record's plaintext is zeroed: each lane its own blocks

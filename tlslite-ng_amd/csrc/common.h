@@ -95,20 +95,38 @@ __device__ __forceinline__ uint32_t bswap32(uint32_t v) {
     return __builtin_bswap32(v);
 }
 
+// p[i] of a global array (batch metadata behind descriptor pointers).
+template <class T>
+__device__ __forceinline__ T gld(const T* p, uint64_t i) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    return ((const __attribute__((address_space(1))) T*)p)[i];
+#else
+    return p[i];
+#endif
+}
+template <class T>
+__device__ __forceinline__ void gst(T* p, uint64_t i, T v) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    ((__attribute__((address_space(1))) T*)p)[i] = v;
+#else
+    p[i] = v;
+#endif
+}
+
 __device__ __forceinline__ const uint8_t* rec_in(const tg_batch& b, uint64_t i) {
-    return b.in + (b.in_off ? b.in_off[i] : i * b.in_stride);
+    return b.in + (b.in_off ? gld(b.in_off, i) : i * b.in_stride);
 }
 __device__ __forceinline__ uint8_t* rec_out(const tg_batch& b, uint64_t i) {
-    return b.out + (b.out_off ? b.out_off[i] : i * b.out_stride);
+    return b.out + (b.out_off ? gld(b.out_off, i) : i * b.out_stride);
 }
 __device__ __forceinline__ uint32_t rec_len(const tg_batch& b, uint64_t i) {
-    return b.len ? b.len[i] : b.fixed_len;
+    return b.len ? gld(b.len, i) : b.fixed_len;
 }
 __device__ __forceinline__ const uint8_t* rec_aad(const tg_batch& b, uint64_t i) {
-    return b.aad + (b.aad_off ? b.aad_off[i] : i * b.aad_stride);
+    return b.aad + (b.aad_off ? gld(b.aad_off, i) : i * b.aad_stride);
 }
 __device__ __forceinline__ uint32_t rec_aad_len(const tg_batch& b, uint64_t i) {
-    return b.aad_len ? b.aad_len[i] : b.fixed_aad_len;
+    return b.aad_len ? gld(b.aad_len, i) : b.fixed_aad_len;
 }
 
 // Record memory is global.  The record pointers come out of the batch
