@@ -190,11 +190,29 @@ __device__ __forceinline__ void stage_quad(uint4* q) {
 // looks up its own column's four bytes -- T0(b0) for column c, T1(b1) for
 // c - 1, T2(b2) for c - 2, T3(b3) for c - 3 (the terms of col()) -- and
 // gathers column c's other three terms from lanes c + 1 .. c + 3 with DPP
-// quad permutes: 4 lookups per round and lane instead of 16 on one lane.
+// quad permutes fused into the XORs: 4 lookups per round and lane instead of
+// 16 on one lane.
+// acc ^ (v of lane (c + K) % 4), one v_xor_b32 with a DPP quad permute on its
+// first operand (the compiler would build v_mov_b32_dpp + v_bitop3 and put
+// two dependent instructions on the chain).  v comes from an LDS read, not a
+// VALU write, so the DPP read needs no wait states.
 template <int K>
-__device__ __forceinline__ uint32_t quad_from(uint32_t v) {   // lane c <- lane (c + K) % 4
-    constexpr int ctrl = K == 1 ? 0x39 : (K == 2 ? 0x4e : 0x93);
-    return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, ctrl, 0xf, 0xf, false);
+__device__ __forceinline__ uint32_t xor_from(uint32_t v, uint32_t acc) {
+    uint32_t d;
+#if defined(__HIP_DEVICE_COMPILE__)
+    if (K == 1)
+        asm volatile("v_xor_b32_dpp %0, %1, %2 quad_perm:[1,2,3,0] row_mask:0xf bank_mask:0xf"
+                     : "=v"(d) : "v"(v), "v"(acc));
+    else if (K == 2)
+        asm volatile("v_xor_b32_dpp %0, %1, %2 quad_perm:[2,3,0,1] row_mask:0xf bank_mask:0xf"
+                     : "=v"(d) : "v"(v), "v"(acc));
+    else
+        asm volatile("v_xor_b32_dpp %0, %1, %2 quad_perm:[3,0,1,2] row_mask:0xf bank_mask:0xf"
+                     : "=v"(d) : "v"(v), "v"(acc));
+#else
+    d = v ^ acc;
+#endif
+    return d;
 }
 
 template <int NR>
@@ -203,10 +221,10 @@ __device__ __forceinline__ uint32_t aes_quad(uint32_t lc, const uint32_t (&rkc)[
 #pragma unroll
     for (int r = 1; r < NR; ++r) {
         const uint32_t p0 = Q<0, 0>(s, lc), p1 = Q<1, 1>(s, lc), p2 = Q<2, 2>(s, lc), p3 = Q<3, 3>(s, lc);
-        s = xor3(p0, quad_from<1>(p1), rkc[r]) ^ xor3(quad_from<2>(p2), quad_from<3>(p3), 0u);
+        s = xor_from<3>(p3, xor_from<2>(p2, xor_from<1>(p1, p0 ^ rkc[r])));
     }
     const uint32_t p0 = Q<4, 0>(s, lc), p1 = Q<5, 1>(s, lc), p2 = Q<6, 2>(s, lc), p3 = Q<7, 3>(s, lc);
-    return xor3(p0, quad_from<1>(p1), rkc[NR]) ^ xor3(quad_from<2>(p2), quad_from<3>(p3), 0u);
+    return xor_from<3>(p3, xor_from<2>(p2, xor_from<1>(p1, p0 ^ rkc[NR])));
 }
 
 // One full block on one lane from the quad table (the stream wave's counter
