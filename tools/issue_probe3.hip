@@ -247,6 +247,44 @@ __global__ void mix_probe(uint32_t* out, uint64_t* cyc, uint32_t seed) {
     if ((threadIdx.x & 63) == 0) cyc[blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64] = t1 - t0;
 }
 
+
+// S independent ChaCha states per thread (column+diagonal double rounds,
+// compiler-scheduled): ILP 4 S per wave.
+template <int R, int S>
+__global__ void chacha_multi_probe(uint32_t* out, uint64_t* cyc, uint32_t seed) {
+    uint32_t x[S][16];
+#pragma unroll
+    for (int q = 0; q < S; ++q)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) x[q][i] = seed * (i + 1) + threadIdx.x + 77 * q;
+    __syncthreads();
+    const uint64_t t0 = __builtin_amdgcn_s_memtime();
+    for (int r = 0; r < R; ++r) {
+#pragma unroll
+        for (int q = 0; q < S; ++q) {
+            QR(x[q][0], x[q][4], x[q][8], x[q][12]);
+            QR(x[q][1], x[q][5], x[q][9], x[q][13]);
+            QR(x[q][2], x[q][6], x[q][10], x[q][14]);
+            QR(x[q][3], x[q][7], x[q][11], x[q][15]);
+        }
+#pragma unroll
+        for (int q = 0; q < S; ++q) {
+            QR(x[q][0], x[q][5], x[q][10], x[q][15]);
+            QR(x[q][1], x[q][6], x[q][11], x[q][12]);
+            QR(x[q][2], x[q][7], x[q][8], x[q][13]);
+            QR(x[q][3], x[q][4], x[q][9], x[q][14]);
+        }
+    }
+    const uint64_t t1 = __builtin_amdgcn_s_memtime();
+    uint32_t acc = 0;
+#pragma unroll
+    for (int q = 0; q < S; ++q)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) acc ^= x[q][i];
+    out[blockIdx.x * blockDim.x + threadIdx.x] = acc;
+    if ((threadIdx.x & 63) == 0) cyc[blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64] = t1 - t0;
+}
+
 static void report(const char* name, int w, float ms, const uint64_t* h, int nw, double instr) {
     double mean = 0;
     for (int i = 0; i < nw; ++i) mean += h[i];
@@ -280,20 +318,11 @@ int main() {
     uint64_t* d_cyc;
     if (hipMalloc(&d_out, 256 * 8 * 256 * 4) != hipSuccess || hipMalloc(&d_cyc, 256 * 8 * 4 * 8) != hipSuccess)
         return 1;
-    const int ws[] = {2, 4, 8};
+    const int ws[] = {2, 3, 4, 6, 8};
     for (int w : ws) {
-        launch("chacha dr (compiler)", chacha_probe<2048, false>, w, 96.0 * 2048, d_out, d_cyc);
-        launch("chacha dr asm alignbit seq", chacha_asm_probe<2048, 0, false>, w, 96.0 * 2048, d_out, d_cyc);
-        launch("chacha dr asm alignbit ilv", chacha_asm_probe<2048, 0, true>, w, 96.0 * 2048, d_out, d_cyc);
-        launch("chacha dr asm shift-or seq", chacha_asm_probe<2048, 1, false>, w, 160.0 * 2048, d_out, d_cyc);
-        launch("chacha dr asm shift-or ilv", chacha_asm_probe<2048, 1, true>, w, 160.0 * 2048, d_out, d_cyc);
-        launch("mix add,xor,alignbit", mix_probe<256>, w, 12.0 * 64 * 256, d_out, d_cyc);
-        launch("lshlrev ILP8", probe<14, 8, 64, 256>, w, 8.0 * 64 * 256, d_out, d_cyc);
-        launch("or ILP8", probe<15, 8, 64, 256>, w, 8.0 * 64 * 256, d_out, d_cyc);
-        launch("pk_add_u16 swap ILP8", probe<16, 8, 64, 256>, w, 8.0 * 64 * 256, d_out, d_cyc);
-        launch("add_co e32 ILP8", probe<17, 8, 64, 256>, w, 8.0 * 64 * 256, d_out, d_cyc);
-        launch("bitop3 vv-inline ILP8", probe<18, 8, 64, 256>, w, 8.0 * 64 * 256, d_out, d_cyc);
-        launch("and ILP8", probe<19, 8, 64, 256>, w, 8.0 * 64 * 256, d_out, d_cyc);
+        launch("chacha 1 state", chacha_multi_probe<1024, 1>, w, 96.0 * 1024, d_out, d_cyc);
+        launch("chacha 2 states", chacha_multi_probe<512, 2>, w, 96.0 * 1024, d_out, d_cyc);
+        launch("chacha 3 states", chacha_multi_probe<342, 3>, w, 96.0 * 1026, d_out, d_cyc);
     }
     return 0;
 }
