@@ -88,6 +88,23 @@ struct KeyPlanesLds {
     }
 };
 
+// The KeyPlanesLds layout in global memory (L1/L2-resident, 1 920 B per
+// key): one vector load per (round, bit) through the vector-memory path,
+// which the octet kernels barely use, so neither the VALU (SGPR operands) nor
+// the LDS (the T-table waves' pipe) pays for the key planes.
+struct KeyPlanesVmem {
+    const uint4* rows;
+    __device__ __forceinline__ uint4 row4(int r, int b) const {
+#if defined(__HIP_DEVICE_COMPILE__)
+        typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+        const v4u v = *(const __attribute__((address_space(1))) v4u*)(rows + 8 * r + b);
+        return make_uint4(v.x, v.y, v.z, v.w);
+#else
+        return rows[8 * r + b];
+#endif
+    }
+};
+
 // Plane (r, i, b) of the (NR + 1) * 32 in ``src`` (GcmKeyDev::bs8mask order)
 // to LDS ``base`` in KeyPlanesLds order; all threads of the workgroup call it.
 __device__ __forceinline__ void stage_lds_planes(uint32_t base, const uint32_t* src, int nr) {

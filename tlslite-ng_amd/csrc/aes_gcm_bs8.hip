@@ -343,19 +343,21 @@ static_assert(kTeBase == 65536, "Te block follows the GHASH tables");
 
 // The batch descriptor is read from memory per job (bp): held in SGPRs
 // across the persistent loop it would crowd out the ciphers' own scalars.
-// LDSKEYS: the bitsliced waves read the round-key planes from LDS (VGPR
-// operands) instead of scalar loads (TLSGPU_HY_KEYS=0 selects it).
-template <int NR, bool OPEN, bool LDSKEYS>
+// KEYS: where the bitsliced waves read the round-key planes -- 1 scalar loads
+// (SGPR operands), 0 LDS, 2 vector loads of the row layout at ``krows``
+// (VGPR operands without LDS traffic); TLSGPU_HY_KEYS selects.
+template <int NR, bool OPEN, int KEYS>
 __global__ __launch_bounds__(kHyThreads) void gcm_hy_kernel(const GcmKeyDev* __restrict__ key,
                                                             const tg_batch* bp,
                                                             const uint32_t* __restrict__ order,
                                                             uint32_t* __restrict__ queue,
-                                                            uint32_t nt, uint32_t prio) {
+                                                            uint32_t nt, uint32_t prio,
+                                                            const uint4* __restrict__ krows) {
     stage_ghash_rot(g_lds_bs8, key->ghash8, kHyJt);
     stage_te(reinterpret_cast<uint32_t*>(g_lds_bs8) + kTeBase / 4);
     stage_sbox(kHySbox);
     if (threadIdx.x < 4 * (NR + 1)) reinterpret_cast<uint32_t*>(g_lds_bs8)[kHyRk / 4 + threadIdx.x] = key->rk[threadIdx.x];
-    if (LDSKEYS) bs8::stage_lds_planes(kHyKeys, key->bs8mask, NR);
+    if (KEYS == 0) bs8::stage_lds_planes(kHyKeys, key->bs8mask, NR);
     __syncthreads();
     const uint32_t wave = (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
     const uint64_t njobs = (bp->n + 7) / 8;
@@ -382,9 +384,12 @@ __global__ __launch_bounds__(kHyThreads) void gcm_hy_kernel(const GcmKeyDev* __r
             if (job >= njobs) break;
             asm volatile("" ::: "memory");
             const tg_batch b = *bp;
-            if (LDSKEYS)
+            if (KEYS == 0)
                 octet_job<NR, OPEN, false>(key, b, order, 8ull * job, recw, none, kHySbox, kHyJt,
                                            bs8::KeyPlanesLds{kHyKeys});
+            else if (KEYS == 2)
+                octet_job<NR, OPEN, false>(key, b, order, 8ull * job, recw, none, kHySbox, kHyJt,
+                                           bs8::KeyPlanesVmem{krows});
             else
                 octet_job<NR, OPEN, false>(key, b, order, 8ull * job, recw, none, kHySbox, kHyJt,
                                            bs8::KeyPlanes{key->bs8mask});
@@ -394,9 +399,16 @@ __global__ __launch_bounds__(kHyThreads) void gcm_hy_kernel(const GcmKeyDev* __r
 
 // Stream-ordered setup of the hybrid kernel's scratch: the job counter and a
 // device copy of the batch descriptor.
-__global__ void hy_setup_kernel(tg_batch b, uint32_t* queue, tg_batch* bcopy) {
-    *queue = 0;
-    *bcopy = b;
+__global__ void hy_setup_kernel(tg_batch b, uint32_t* queue, tg_batch* bcopy,
+                                const GcmKeyDev* __restrict__ key, uint32_t* krows, int nr) {
+    if (threadIdx.x == 0) {
+        *queue = 0;
+        *bcopy = b;
+    }
+    for (int e = threadIdx.x; e < 32 * (nr + 1); e += blockDim.x) {   // KeyPlanesVmem layout
+        const int r = e >> 5, i = (e >> 3) & 3, bit = e & 7;
+        krows[4 * (8 * r + bit) + i] = key->bs8mask[e];
+    }
 }
 
 template <int NR, bool OPEN>
@@ -415,12 +427,12 @@ int launch_bs8(const GcmKeyDev* key, const tg_batch& b, hipStream_t s, const uin
     return hipGetLastError() == hipSuccess ? TG_OK : TG_EHIP;
 }
 
-template <int NR, bool OPEN, bool LDSKEYS>
+template <int NR, bool OPEN, int KEYS>
 int launch_hy_k(const GcmKeyDev* key, const tg_batch& b, hipStream_t s, const uint32_t* order,
                 uint32_t nt, uint32_t prio) {
     static bool attr_set = false;
     if (!attr_set) {
-        if (hipFuncSetAttribute((const void*)gcm_hy_kernel<NR, OPEN, LDSKEYS>,
+        if (hipFuncSetAttribute((const void*)gcm_hy_kernel<NR, OPEN, KEYS>,
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)kHyLds) != hipSuccess)
             return TG_EHIP;
         attr_set = true;
@@ -428,14 +440,16 @@ int launch_hy_k(const GcmKeyDev* key, const tg_batch& b, hipStream_t s, const ui
     // job counter + batch copy: stream-ordered scratch, so concurrent batches
     // never share them
     uint8_t* scratch = nullptr;
-    if (hipMallocAsync((void**)&scratch, 256, s) != hipSuccess) return TG_EHIP;
+    if (hipMallocAsync((void**)&scratch, 256 + 2048, s) != hipSuccess) return TG_EHIP;
     uint32_t* queue = reinterpret_cast<uint32_t*>(scratch);
     tg_batch* bcopy = reinterpret_cast<tg_batch*>(scratch + 64);
-    hipLaunchKernelGGL(hy_setup_kernel, dim3(1), dim3(1), 0, s, b, queue, bcopy);
+    uint32_t* krows = reinterpret_cast<uint32_t*>(scratch + 256);
+    hipLaunchKernelGGL(hy_setup_kernel, dim3(1), dim3(64), 0, s, b, queue, bcopy, key, krows, NR);
     bool ok = hipGetLastError() == hipSuccess;
     if (ok) {
-        hipLaunchKernelGGL((gcm_hy_kernel<NR, OPEN, LDSKEYS>), dim3((unsigned)device_cus()), dim3(kHyThreads),
-                           kHyLds, s, key, (const tg_batch*)bcopy, order, queue, nt, prio);
+        hipLaunchKernelGGL((gcm_hy_kernel<NR, OPEN, KEYS>), dim3((unsigned)device_cus()), dim3(kHyThreads),
+                           kHyLds, s, key, (const tg_batch*)bcopy, order, queue, nt, prio,
+                           (const uint4*)krows);
         ok = hipGetLastError() == hipSuccess;
     }
     if (hipFreeAsync(scratch, s) != hipSuccess) return TG_EHIP;
@@ -454,8 +468,10 @@ int launch_hy(const GcmKeyDev* key, const tg_batch& b, hipStream_t s, const uint
     const char* ek = getenv("TLSGPU_HY_KEYS");
     const uint32_t nt = et ? (uint32_t)atoi(et) : 8u;
     const uint32_t prio = ep ? (uint32_t)atoi(ep) : 1u;
-    if (ek && atoi(ek) == 0) return launch_hy_k<NR, OPEN, true>(key, b, s, order, nt, prio);
-    return launch_hy_k<NR, OPEN, false>(key, b, s, order, nt, prio);
+    const int keys = ek ? atoi(ek) : 1;
+    if (keys == 0) return launch_hy_k<NR, OPEN, 0>(key, b, s, order, nt, prio);
+    if (keys == 2) return launch_hy_k<NR, OPEN, 2>(key, b, s, order, nt, prio);
+    return launch_hy_k<NR, OPEN, 1>(key, b, s, order, nt, prio);
 }
 
 }  // namespace
