@@ -72,6 +72,21 @@ def test_forced_kernel_vs_oracle(torch, tg, oracle_mod, alg, klen, var, value, a
                       tamper=(1, 30, 111))
 
 
+@pytest.mark.parametrize("keys", ["0", "2"])          # key planes from LDS / vector loads
+@pytest.mark.parametrize("klen", [16, 32])
+def test_hybrid_key_plane_sources(torch, tg, oracle_mod, keys, klen, monkeypatch):
+    """The hybrid kernel's alternative key-plane providers (TLSGPU_HY_KEYS)."""
+    from batchpack import HostBatch, run_seal_open
+    rng = np.random.default_rng(300 + klen + int(keys))
+    lens = LENS * 3 + list(rng.integers(0, 16401, 60)) + [65536, 70001]
+    hb = HostBatch(lens, payload_seed=31, align=16, aad_mode="random")
+    key = rng.bytes(klen)
+    monkeypatch.setenv("TLSGPU_GCM_VARIANT", "15")
+    monkeypatch.setenv("TLSGPU_HY_KEYS", keys)
+    run_seal_open(torch, tg, oracle_mod, hb, "aesgcm", np.frombuffer(key, np.uint8),
+                  tg.HipAESGCM(bytearray(key)), tamper=(2, 40))
+
+
 @pytest.mark.parametrize("alg,klen", [("aesgcm", 16), ("chacha", 32)])
 def test_auto_wave_per_record_batch(torch, tg, oracle_mod, alg, klen):
     """A 2048-record batch (four waves per record for AES-GCM, one for ChaCha)."""
