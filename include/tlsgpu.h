@@ -239,7 +239,8 @@ int tg_gather(const uint8_t* src, const uint64_t* src_off, const uint32_t* len, 
  *   order); mode 0 = 8-bit tables, 1 = 8-bit tables 8 rows in flight,
  *   2 = conflict-free rotated tables, 3 = table-free carry-less multiply,
  *   4 = octet stride-H^8 + lift (aes_gcm_bs8.hip), 5 = wave stride-H^64 +
- *   lift (gcm_wave_kernel). */
+ *   lift (gcm_wave_kernel), 6 = octet stride-H^8 through a wave's 4-bit
+ *   tables (the key-table octet kernel). */
 int tg_selftest_poly1305(int mode, const uint8_t* keys, const uint8_t* msgs, const uint64_t* off,
                          const uint32_t* len, uint64_t n, uint8_t* tags);
 int tg_selftest_ghash(int mode, const uint8_t* h, const uint8_t* aad, const uint64_t* aad_off,

@@ -10,9 +10,11 @@ import pytest
 pytestmark = pytest.mark.gpu
 
 
-def test_config4_full_shape_sampled(oracle_mod):
+@pytest.mark.parametrize("variant", ["0", "14"])   # lane kernel / key-grouped octet kernel
+def test_config4_full_shape_sampled(oracle_mod, variant, monkeypatch):
     import torch
     import tlsgpu
+    monkeypatch.setenv("TLSGPU_GCM_TABLE_VARIANT", variant)
     if not torch.cuda.is_available():
         pytest.fail("GPU tests need a visible MI355X")
     n, nkeys = 1 << 20, 65536

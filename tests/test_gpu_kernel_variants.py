@@ -192,3 +192,22 @@ def test_key_table_wave_kernel(torch, tg, oracle_mod, klen, threads, align):
     with _with_env("TLSGPU_GCM_TABLE_WAVE_THREADS", threads), \
             _with_env("TLSGPU_GCM_TABLE_VARIANT", "5"):
         run_seal_open(torch, tg, oracle_mod, hb, "aesgcm", karr, obj, tamper=(4, 100, len(lens) - 1))
+
+
+@pytest.mark.parametrize("klen", [16, 32])
+@pytest.mark.parametrize("keys", [2, 37, 300])
+@pytest.mark.parametrize("align", [16, 1])
+def test_key_table_octet_kernel(torch, tg, oracle_mod, klen, keys, align, monkeypatch):
+    """Many keys, ragged lengths, through the key-grouped octet kernel
+    (aes_gcm_bs8.hip gcm_kt_kernel, TLSGPU_GCM_TABLE_VARIANT=14): jobs of at
+    most eight records of one key, bitsliced keystream with the key's planes,
+    GHASH through the wave's 4-bit tables of the key's H^8."""
+    from batchpack import HostBatch, run_seal_open
+    rng = np.random.default_rng(700 + klen + keys + align)
+    lens = LENS * 4 + list(rng.integers(0, 16401, 400)) + [20000, 65000, 70001]
+    hb = HostBatch(lens, payload_seed=align + 91, align=align, aad_mode="random", key_count=keys)
+    kb = [rng.bytes(klen) for _ in range(keys)]
+    obj = tg.KeyTable("aesgcm", kb)
+    karr = np.frombuffer(b"".join(kb), np.uint8).reshape(keys, klen)
+    monkeypatch.setenv("TLSGPU_GCM_TABLE_VARIANT", "14")
+    run_seal_open(torch, tg, oracle_mod, hb, "aesgcm", karr, obj, tamper=(4, 100, len(lens) - 1))

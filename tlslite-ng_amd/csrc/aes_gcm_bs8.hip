@@ -120,17 +120,36 @@ __device__ __forceinline__ void t_half(uint32_t lane4, const RkLds& rk, const Ct
                            col_last(s[q][3], s[q][0], s[q][1], s[q][2], k.w, lane4));
 }
 
+// Key contexts of octet_job: the round-key words (GcmKeyDev / GcmTableKey
+// ``rk`` layout), H^e in normal order for the lift, and y * H^8 for the
+// stride-8 Horner.
+struct SingleKeyCtx {   // one key for the batch: 8-bit H^8 tables in LDS (gmul_rot)
+    const GcmKeyDev* key;
+    uint32_t jt;
+    __device__ __forceinline__ const uint32_t* rk() const { return key->rk; }
+    __device__ __forceinline__ uint4 hpow(int e) const { return key->hpow[e - 1]; }
+    __device__ __forceinline__ uint4 gmul(uint4 y) const { return gmul_rot(y, threadIdx.x & 15u, jt); }
+};
+struct TableKeyCtx {    // a key of a key table: the wave's 4-bit H^8 tables in LDS (gmul4)
+    const uint32_t* rkw;
+    const uint4* hp;    // H^1 .. H^64 of this key (tg_launch_table_hpow)
+    uint32_t tab;
+    __device__ __forceinline__ const uint32_t* rk() const { return rkw; }
+    __device__ __forceinline__ uint4 hpow(int e) const { return hp[e - 1]; }
+    __device__ __forceinline__ uint4 gmul(uint4 y) const { return gmul4(y, tab); }
+};
+
 // One octet job: the eight records of record slots t0 .. t0 + 7 on this wave
 // (lane 8 q + l = lane l of slot t0 + q).  TROLE: the keystream comes from the
 // T-table cipher (aes_round.h, Te tables at kTeBase, round keys in SGPRs)
 // instead of the bitsliced one; everything else is shared.  ``recb``: this
 // wave's 1 KiB of LDS for the records' first-state planes.
-template <int NR, bool OPEN, bool TROLE, class KM>
-__device__ __forceinline__ void octet_job(const GcmKeyDev* __restrict__ key, const tg_batch& b,
+template <int NR, bool OPEN, bool TROLE, class KM, class KC>
+__device__ __forceinline__ void octet_job(const KC& kc, const tg_batch& b,
                                           const uint32_t* __restrict__ order, uint64_t t0,
                                           uint32_t recw, const RkLds& rkT, uint32_t sbox,
-                                          uint32_t jt, const KM& km) {
-    const uint32_t* rk = key->rk;
+                                          const KM& km) {
+    const uint32_t* rk = kc.rk();
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t l = lane & 7u;
     const uint64_t t = t0 + (lane >> 3);
@@ -174,7 +193,7 @@ __device__ __forceinline__ void octet_job(const GcmKeyDev* __restrict__ key, con
     uint4 y = make_uint4(0, 0, 0, 0);
     for (uint32_t a = (l + na + nc + 1u) & 7u; a < na; a += 8) {
         const uint32_t m = alen - 16 * a < 16 ? alen - 16 * a : 16;
-        y = xor4(gmul_rot(y, lane & 15u, jt), load_partial(ad + 16 * a, m));
+        y = xor4(kc.gmul(y), load_partial(ad + 16 * a, m));
     }
 
     // the bitsliced cipher leaves out the last round key (folded into the XOR)
@@ -200,7 +219,7 @@ __device__ __forceinline__ void octet_job(const GcmKeyDev* __restrict__ key, con
                     if (!OPEN) d[q] = c;
                 }
 #pragma unroll
-                for (int q = 0; q < N; ++q) y = xor4(gmul_rot(y, lane & 15u, jt), d[q]);
+                for (int q = 0; q < N; ++q) y = xor4(kc.gmul(y), d[q]);
             }
         } else {
 #pragma unroll
@@ -219,7 +238,7 @@ __device__ __forceinline__ void octet_job(const GcmKeyDev* __restrict__ key, con
                     c = mask_tail(xor4(d, kk), tail);
                     store_partial(out + 16u * blk, c, tail);
                 }
-                y = xor4(gmul_rot(y, lane & 15u, jt), OPEN ? d : c);
+                y = xor4(kc.gmul(y), OPEN ? d : c);
             }
         }
     };
@@ -267,12 +286,12 @@ __device__ __forceinline__ void octet_job(const GcmKeyDev* __restrict__ key, con
     // length block be64(8 alen) || be64(8 len) (aesgcm.py:64): the last position
     if (l == 7) {
         const uint64_t abits = (uint64_t)alen << 3, cbits = (uint64_t)len << 3;
-        y = xor4(gmul_rot(y, lane & 15u, jt), make_uint4(bswap32((uint32_t)(abits >> 32)), bswap32((uint32_t)abits),
+        y = xor4(kc.gmul(y), make_uint4(bswap32((uint32_t)(abits >> 32)), bswap32((uint32_t)abits),
                                      bswap32((uint32_t)(cbits >> 32)), bswap32((uint32_t)cbits)));
     }
     // lift by H^(8 - l) and XOR-reduce over the octet
     uint4 yn = norm4(y);
-    if (yn.x | yn.y | yn.z | yn.w) yn = gf128_mul(yn, key->hpow[7 - l]);
+    if (yn.x | yn.y | yn.z | yn.w) yn = gf128_mul(yn, kc.hpow(8 - l));
 #pragma unroll
     for (int m = 1; m < 8; m <<= 1) yn = xor4(yn, shfl_xor4(yn, m));
     // tag = GHASH ^ E_K(J0), J0 = nonce || be32(1) (aesgcm.py:112-122)
@@ -319,8 +338,9 @@ __global__ __launch_bounds__(kBs8Threads, 4) void gcm_bs8_kernel(const GcmKeyDev
     bs8::stage_lds_planes(kBs8Keys, key->bs8mask, NR);
     __syncthreads();
     const uint32_t wave = threadIdx.x >> 6;
-    octet_job<NR, OPEN, false>(key, b, order, (uint64_t)blockIdx.x * kBs8Recs + 8u * wave,
-                               kBs8RecBase + wave * 1024u, RkLds{0}, kBs8Sbox, kBs8Jt,
+    octet_job<NR, OPEN, false>(SingleKeyCtx{key, kBs8Jt}, b, order,
+                               (uint64_t)blockIdx.x * kBs8Recs + 8u * wave,
+                               kBs8RecBase + wave * 1024u, RkLds{0}, kBs8Sbox,
                                bs8::KeyPlanesLds{kBs8Keys});
 }
 
@@ -372,8 +392,8 @@ __global__ __launch_bounds__(kHyThreads) void gcm_hy_kernel(const GcmKeyDev* __r
             if (job >= njobs) break;
             asm volatile("" ::: "memory");
             const tg_batch b = *bp;
-            octet_job<NR, OPEN, true>(key, b, order, 8ull * job, recw, rk, kHySbox, kHyJt,
-                                      bs8::KeyPlanesLds{kHyKeys});
+            octet_job<NR, OPEN, true>(SingleKeyCtx{key, kHyJt}, b, order, 8ull * job, recw, rk,
+                                      kHySbox, bs8::KeyPlanesLds{kHyKeys});
         }
     } else {
         const RkLds none{0};
@@ -385,14 +405,14 @@ __global__ __launch_bounds__(kHyThreads) void gcm_hy_kernel(const GcmKeyDev* __r
             asm volatile("" ::: "memory");
             const tg_batch b = *bp;
             if (KEYS == 0)
-                octet_job<NR, OPEN, false>(key, b, order, 8ull * job, recw, none, kHySbox, kHyJt,
-                                           bs8::KeyPlanesLds{kHyKeys});
+                octet_job<NR, OPEN, false>(SingleKeyCtx{key, kHyJt}, b, order, 8ull * job, recw,
+                                           none, kHySbox, bs8::KeyPlanesLds{kHyKeys});
             else if (KEYS == 2)
-                octet_job<NR, OPEN, false>(key, b, order, 8ull * job, recw, none, kHySbox, kHyJt,
-                                           bs8::KeyPlanesVmem{krows});
+                octet_job<NR, OPEN, false>(SingleKeyCtx{key, kHyJt}, b, order, 8ull * job, recw,
+                                           none, kHySbox, bs8::KeyPlanesVmem{krows});
             else
-                octet_job<NR, OPEN, false>(key, b, order, 8ull * job, recw, none, kHySbox, kHyJt,
-                                           bs8::KeyPlanes{key->bs8mask});
+                octet_job<NR, OPEN, false>(SingleKeyCtx{key, kHyJt}, b, order, 8ull * job, recw,
+                                           none, kHySbox, bs8::KeyPlanes{key->bs8mask});
         }
     }
 }
@@ -474,6 +494,97 @@ int launch_hy(const GcmKeyDev* key, const tg_batch& b, hipStream_t s, const uint
     return launch_hy_k<NR, OPEN, 1>(key, b, s, order, nt, prio);
 }
 
+// ---- key tables: key-grouped octet jobs on bitsliced waves ----------------
+// A batch over a key table (config 4: many sessions, per-record key_idx) is
+// planned into jobs of at most eight records of ONE key (tg_key_job_plan:
+// sorted by key, then length descending).  A wave's job then has
+// wave-uniform round keys and key planes (scalar loads from the key table and
+// the per-key plane table) and one GHASH key: the wave builds 4-bit tables of
+// that key's H^8 in its own 8 KiB of LDS (build_table4, ~700 VALU per lane;
+// gmul4: 32 conflict-free lookups per block instead of the table-free
+// multiply's ~650 VALU slots).  No Te tables (the LDS holds the GHASH
+// copies), so every wave runs the bitsliced cipher.
+//
+// One job per wave, four waves per workgroup, no persistent loop: the jobs of
+// a key are consecutive, so a persistent wave would rarely keep its key, and
+// a loop around the job body made the compiler hoist its per-lane table and
+// plane addresses and spill ~180 VGPRs.  The grid is sized for the most jobs
+// a batch of n records can have (n / 8 rounded up per key: at most n); waves
+// past the planned count exit at once.
+constexpr int kKtThreads = 256;
+constexpr int kKtWaves = kKtThreads / 64;
+constexpr uint32_t kKtSbox = kKtWaves * 8192;            // after the per-wave tables
+constexpr uint32_t kKtRecBase = kKtSbox + 256;           // 1 KiB of record planes per wave
+constexpr size_t kKtLds = kKtRecBase + kKtWaves * 1024;
+constexpr int kKtPlaneWords = 15 * 32;                   // per key in the plane table
+
+template <int NR, bool OPEN>
+__global__ __launch_bounds__(kKtThreads, 4) void gcm_kt_kernel(const GcmTableKey* __restrict__ keys,
+                                                            const uint4* __restrict__ hpow,
+                                                            const uint32_t* __restrict__ planes,
+                                                            tg_batch b,
+                                                            const uint32_t* __restrict__ order,
+                                                            const uint32_t* __restrict__ jobpos,
+                                                            const uint32_t* __restrict__ njobs_p) {
+    stage_sbox(kKtSbox);
+    __syncthreads();
+    const uint32_t wave = (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    const uint32_t job = blockIdx.x * kKtWaves + wave;
+    if (job >= *njobs_p) return;
+    const uint32_t tab = 8192u * wave, recw = kKtRecBase + wave * 1024u;
+    const uint32_t p0 = gld(jobpos, job), p1 = gld(jobpos, job + 1);
+    const uint32_t k = (uint32_t)__builtin_amdgcn_readfirstlane((int)gld(b.key_idx, gld(order, p0)));
+    build_table4(tab, hpow[64u * k + 7u]);   // this wave's GHASH tables for the job's key
+    __builtin_amdgcn_wave_barrier();
+    b.n = p1;   // the job's slots are p0 .. p1 - 1 (at most eight)
+    octet_job<NR, OPEN, false>(TableKeyCtx{keys[k].rk, hpow + 64u * k, tab}, b, order, p0, recw,
+                               RkLds{0}, kKtSbox, bs8::KeyPlanes{planes + kKtPlaneWords * k});
+}
+
+__global__ void kt_planes_kernel(const GcmTableKey* __restrict__ keys, uint64_t n, int nr,
+                                 uint32_t* __restrict__ planes) {
+    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const uint64_t k = t / kKtPlaneWords;
+    const int e = (int)(t % kKtPlaneWords);
+    if (k >= n) return;
+    planes[t] = e < 32 * (nr + 1) ? bs8_mask_word(keys[k].rk, e) : 0u;
+}
+
+template <int NR, bool OPEN>
+int launch_kt(const GcmTableKey* keys, const uint4* hpow, const uint32_t* planes, const tg_batch& b,
+              hipStream_t s) {
+    static bool attr_set = false;
+    if (!attr_set) {
+        if (hipFuncSetAttribute((const void*)gcm_kt_kernel<NR, OPEN>,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)kKtLds) != hipSuccess)
+            return TG_EHIP;
+        attr_set = true;
+    }
+    if (b.n == 0) return TG_OK;
+    if (b.n > 0xfffffffeull || !b.key_idx) return TG_EINVAL;
+    size_t plan = 0;
+    int rc = tg_key_job_plan(b.key_idx, b.len, b.fixed_len, b.n, nullptr, nullptr, nullptr, nullptr,
+                             &plan, s);
+    if (rc) return rc;
+    const size_t so = (b.n * 4 + 255) & ~(size_t)255, sj = ((b.n + 1) * 4 + 255) & ~(size_t)255;
+    uint8_t* buf = nullptr;
+    if (hipMallocAsync((void**)&buf, so + sj + 256 + plan, s) != hipSuccess) return TG_EHIP;
+    uint32_t* order = reinterpret_cast<uint32_t*>(buf);
+    uint32_t* jobpos = reinterpret_cast<uint32_t*>(buf + so);
+    uint32_t* njobs = reinterpret_cast<uint32_t*>(buf + so + sj);
+    rc = tg_key_job_plan(b.key_idx, b.len, b.fixed_len, b.n, order, jobpos, njobs, buf + so + sj + 256,
+                         &plan, s);
+    if (!rc) {
+        const uint64_t groups = (b.n + kKtWaves - 1) / kKtWaves;   // njobs <= n
+        hipLaunchKernelGGL((gcm_kt_kernel<NR, OPEN>), dim3((unsigned)groups), dim3(kKtThreads), kKtLds, s,
+                           keys, hpow, planes, b, (const uint32_t*)order, (const uint32_t*)jobpos,
+                           (const uint32_t*)njobs);
+        rc = hipGetLastError() == hipSuccess ? TG_OK : TG_EHIP;
+    }
+    if (hipFreeAsync(buf, s) != hipSuccess) return TG_EHIP;
+    return rc;
+}
+
 }  // namespace
 }  // namespace tg
 
@@ -493,4 +604,23 @@ int tg_launch_gcm_bs8(const tg::GcmKeyDev* key, int rounds, const tg_batch& b, b
     if (rounds == 14)
         return open ? tg::launch_bs8<14, true>(key, b, s, order) : tg::launch_bs8<14, false>(key, b, s, order);
     return TG_EINVAL;
+}
+
+int tg_launch_gcm_kt(const tg::GcmTableKey* keys, const uint4* hpow, const uint32_t* planes, int rounds,
+                     const tg_batch& b, bool open, hipStream_t s) {
+    if (rounds == 10)
+        return open ? tg::launch_kt<10, true>(keys, hpow, planes, b, s)
+                    : tg::launch_kt<10, false>(keys, hpow, planes, b, s);
+    if (rounds == 14)
+        return open ? tg::launch_kt<14, true>(keys, hpow, planes, b, s)
+                    : tg::launch_kt<14, false>(keys, hpow, planes, b, s);
+    return TG_EINVAL;
+}
+
+int tg_launch_kt_planes(const tg::GcmTableKey* keys, uint64_t n, int rounds, uint32_t* planes,
+                        hipStream_t s) {
+    const uint64_t total = n * tg::kKtPlaneWords;
+    hipLaunchKernelGGL(tg::kt_planes_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, keys, n,
+                       rounds, planes);
+    return hipGetLastError() == hipSuccess ? TG_OK : TG_EHIP;
 }

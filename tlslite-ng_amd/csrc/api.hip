@@ -100,17 +100,40 @@ int ensure_stage(tg_key* k, size_t bytes) {
 bool is_ccm(int alg) { return alg == TG_AES_CCM || alg == TG_AES_CCM_8; }
 
 // A multi-key AES-GCM allocation: GcmTableKey[nkeys], then the 64 GHASH
-// powers of each key (gcm_table_wave_kernel).
+// powers of each key (gcm_table_wave_kernel, gcm_kt_kernel), then the 15 x 32
+// bitsliced round-key planes of each key (gcm_kt_kernel).
 constexpr size_t kTableHpowBytes = 64 * sizeof(uint4);
+constexpr size_t kTablePlaneBytes = 15 * 32 * sizeof(uint32_t);
 uint4* table_hpow(const tg_key* k) {
     return reinterpret_cast<uint4*>(static_cast<uint8_t*>(k->dev_key) +
                                     sizeof(tg::GcmTableKey) * k->nkeys);
+}
+uint32_t* table_planes(const tg_key* k) {
+    return reinterpret_cast<uint32_t*>(reinterpret_cast<uint8_t*>(table_hpow(k)) +
+                                       kTableHpowBytes * k->nkeys);
+}
+
+// Key-table AES-GCM batches above the wave-per-record sizes run the
+// key-grouped octet kernel (aes_gcm_bs8.hip gcm_kt_kernel, its own planner)
+// when TLSGPU_GCM_TABLE_VARIANT is 14, the lane kernel otherwise; 14 also
+// forces it for small batches (tests).
+int kt_choice() {
+    const char* e = getenv("TLSGPU_GCM_TABLE_VARIANT");
+    return e ? atoi(e) : -1;
+}
+
+// The table's derived arrays on the device: H^1..H^64 and the key planes.
+int table_derive(tg_key* k, hipStream_t s) {
+    const auto* keys = static_cast<const tg::GcmTableKey*>(k->dev_key);
+    int rc = tg_launch_table_hpow(keys, k->nkeys, table_hpow(k), s);
+    if (!rc) rc = tg_launch_kt_planes(keys, k->nkeys, k->rounds, table_planes(k), s);
+    return rc;
 }
 
 size_t dev_key_bytes(const tg_key* k) {
     if (k->alg == TG_CHACHA20_POLY1305) return sizeof(tg::ChachaKeyDev) * k->nkeys;
     if (is_ccm(k->alg)) return sizeof(tg::AesKeyDev) * k->nkeys;
-    return k->nkeys > 1 ? (sizeof(tg::GcmTableKey) + kTableHpowBytes) * k->nkeys
+    return k->nkeys > 1 ? (sizeof(tg::GcmTableKey) + kTableHpowBytes + kTablePlaneBytes) * k->nkeys
                         : sizeof(tg::GcmKeyDev);
 }
 
@@ -130,7 +153,8 @@ int launch(tg_key* k, const tg_batch& b, bool open, hipStream_t s) {
     const bool wave = k->nkeys == 1 ? ((k->alg == TG_AES_GCM && tg_gcm_wave_path(b.n)) ||
                                        (k->alg == TG_CHACHA20_POLY1305 && tg_chacha_wave_path(b.n)))
                                     : k->alg == TG_AES_GCM && tg_gcm_table_wave_path(b.n);
-    if (!b.len || b.n < kPlanMinRecords || wave || is_ccm(k->alg) || b.n > 0xffffffffull ||
+    const bool kt = k->alg == TG_AES_GCM && k->nkeys > 1 && kt_choice() == 14;   // plans its own jobs
+    if (!b.len || b.n < kPlanMinRecords || wave || kt || is_ccm(k->alg) || b.n > 0xffffffffull ||
         (e && atoi(e)))
         return launch_kernels(k, b, open, s, nullptr);
     size_t scratch = 0;
@@ -150,6 +174,9 @@ int launch_kernels(tg_key* k, const tg_batch& b, bool open, hipStream_t s, const
     if (is_ccm(k->alg))
         return tg_launch_ccm(static_cast<const tg::AesKeyDev*>(k->dev_key), k->nkeys > 1,
                              k->rounds, k->taglen, b, open, s);
+    if (k->alg == TG_AES_GCM && k->nkeys > 1 && !order && kt_choice() == 14)
+        return tg_launch_gcm_kt(static_cast<const tg::GcmTableKey*>(k->dev_key), table_hpow(k),
+                                table_planes(k), k->rounds, b, open, s);
     if (k->alg == TG_AES_GCM && k->nkeys > 1)
         return tg_launch_gcm_table(static_cast<const tg::GcmTableKey*>(k->dev_key), table_hpow(k),
                                    k->rounds, b, open, s, order);
@@ -445,9 +472,7 @@ int tg_key_create(int alg, const uint8_t* keys, size_t keylen, size_t nkeys, tg_
             e = hipMalloc(&k->dev_key, dev_key_bytes(k));
             if (e == hipSuccess) e = hipMemcpy(k->dev_key, hk, bytes, hipMemcpyHostToDevice);
             if (e != hipSuccess) rc = fail(TG_EHIP, "key upload: %s", hipGetErrorString(e));
-            if (!rc && tg_launch_table_hpow(static_cast<const tg::GcmTableKey*>(k->dev_key), nkeys,
-                                            table_hpow(k), nullptr))
-                rc = fail(TG_EHIP, "key powers launch failed");
+            if (!rc && table_derive(k, nullptr)) rc = fail(TG_EHIP, "key powers launch failed");
             if (!rc && (e = hipDeviceSynchronize()) != hipSuccess)
                 rc = fail(TG_EHIP, "key powers: %s", hipGetErrorString(e));
             memset(hk, 0, sizeof(tg::GcmTableKey) * nkeys);
@@ -504,9 +529,7 @@ int tg_key_create_device(int alg, const uint8_t* keys, size_t keylen, size_t nke
     } else {
         const int layout = is_ccm(alg) ? 2 : (nkeys > 1 ? 1 : 0);
         rc = tg_launch_aes_setup((int)keylen, layout, keys, nkeys, k->dev_key, st);
-        if (!rc && layout == 1)
-            rc = tg_launch_table_hpow(static_cast<const tg::GcmTableKey*>(k->dev_key), nkeys,
-                                      table_hpow(k), st);
+        if (!rc && layout == 1) rc = table_derive(k, st);
         if (rc) rc = fail(rc, "key setup launch failed");
     }
     if (!rc && (e = hipStreamSynchronize(st)) != hipSuccess)

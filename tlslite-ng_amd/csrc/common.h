@@ -246,6 +246,16 @@ int tg_launch_table_hpow(const tg::GcmTableKey* keys, uint64_t n, uint4* hpow, h
 bool tg_gcm_table_wave_path(uint64_t n);
 int tg_length_order(const uint32_t* len, uint64_t n, uint32_t* order, void* scratch, size_t* bytes,
                     hipStream_t s);
+// Key-grouped octet jobs of a key-table batch (planner.hip).
+int tg_key_job_plan(const uint32_t* key_idx, const uint32_t* len, uint32_t fixed_len, uint64_t n,
+                    uint32_t* order, uint32_t* jobpos, uint32_t* njobs, void* scratch, size_t* bytes,
+                    hipStream_t s);
+// The key-table octet kernel (aes_gcm_bs8.hip): planes = per-key bitsliced
+// round-key planes (tg_launch_kt_planes), hpow = the keys' H^1..H^64.
+int tg_launch_gcm_kt(const tg::GcmTableKey* keys, const uint4* hpow, const uint32_t* planes, int rounds,
+                     const tg_batch& b, bool open, hipStream_t s);
+int tg_launch_kt_planes(const tg::GcmTableKey* keys, uint64_t n, int rounds, uint32_t* planes,
+                        hipStream_t s);
 int tg_launch_ccm(const tg::AesKeyDev* keys, bool table, int rounds, int taglen,
                   const tg_batch& b, bool open, hipStream_t s);
 // Whether a single-key batch of n records runs the wave-per-record kernel

@@ -202,6 +202,76 @@ __device__ __forceinline__ uint4 gf128_pow(uint4 x, uint32_t e) {
     return r;
 }
 
+// ---- 4-bit tables of one key's H^8, one copy per wave (key-table octet
+// kernel) ----------------------------------------------------------------
+// Entry (j, n) at tab + 256 j + 16 n = n x^(4j) G in the 8-bit tables' byte
+// layout: nibble j is the high (j even) or low (j odd) nibble of byte j / 2,
+// so M4[2B][n] = M_B[n << 4] and M4[2B + 1][n] = M_B[n].  A 16-entry table is
+// 256 B, all 64 banks once: a wave's lookups into one table never conflict.
+// 8 KiB per copy; tab must be 256-byte aligned.
+//
+// In GCM bit order bit 0x80 >> m of byte B is the coefficient of x^(8B + m),
+// so M4[j][n] = XOR over k = 0..3 with n & (8 >> k) of x^(4j + k) G.  Lane
+// (j, half) of the wave (j = lane % 32) builds the basis x^(4j) G with one
+// table-free multiply by the monomial, x^(4j+1..3) G by shifts, and writes
+// the eight entries n = 8 half .. 8 half + 7 of table j: ~700 VALU per lane
+// when a wave's key changes.  gn: G in normal order (a key's H^8 from its
+// power table).
+__device__ __forceinline__ uint4 gf128_mulx(uint4 v) {   // v * x, normal order
+    const uint32_t c = v.w >> 31;
+    return make_uint4((v.x << 1) ^ (c * 0x87u), __builtin_amdgcn_alignbit(v.y, v.x, 31),
+                      __builtin_amdgcn_alignbit(v.z, v.y, 31), __builtin_amdgcn_alignbit(v.w, v.z, 31));
+}
+
+__device__ __forceinline__ void build_table4(uint32_t tab, uint4 gn) {
+    const uint32_t lane = threadIdx.x & 63u, j = lane & 31u, n0 = (lane >> 5) * 8u;
+    const uint32_t s = 4u * j, bit = 1u << (s & 31u), q = s >> 5;
+    const uint4 mono = make_uint4(q == 0 ? bit : 0u, q == 1 ? bit : 0u, q == 2 ? bit : 0u, q == 3 ? bit : 0u);
+    uint4 bas[4];
+    bas[0] = gf128_mul(gn, mono);
+    bas[1] = gf128_mulx(bas[0]);
+    bas[2] = gf128_mulx(bas[1]);
+    bas[3] = gf128_mulx(bas[2]);
+#pragma unroll
+    for (uint32_t n = 0; n < 8; ++n) {
+        const uint32_t nn = n0 + n;
+        uint4 v = make_uint4(0, 0, 0, 0);
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+            if (nn & (8u >> k)) v = xor4(v, bas[k]);
+        lds_st128(tab + 256u * j + 16u * nn, norm4(v));
+    }
+}
+
+// y * G through the 4-bit tables at ``tab`` (32 lookups, no reduction).
+// tab must be 256-byte aligned (the nibble offsets are ORed in).
+__device__ __forceinline__ uint4 gmul4(uint4 y, uint32_t tab) {
+    const uint32_t w[4] = {y.x, y.y, y.z, y.w};
+    uint4 z = make_uint4(0, 0, 0, 0);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        uint4 e[8];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const uint32_t B = 4 * q + k;
+            const uint32_t hi = k ? (w[q] >> (8 * k)) & 0xf0u : w[q] & 0xf0u;
+            const uint32_t lo = k ? (w[q] >> (8 * k - 4)) & 0xf0u : (w[q] << 4) & 0xf0u;
+            // (nibble | tab) + constant: the constant rides in the ds_read
+            // offset field and nothing table-shaped is loop-invariant
+            e[2 * k] = lds_u128((hi | tab) + 512u * B);
+            e[2 * k + 1] = lds_u128((lo | tab) + 512u * B + 256u);
+        }
+        z = xor4_3(z, e[0], e[1]);
+        z = xor4_3(z, e[2], e[3]);
+        z = xor4_3(z, e[4], e[5]);
+        z = xor4_3(z, e[6], e[7]);
+        // eight rows in flight (32 VGPRs): z is made opaque per group, or
+        // the XOR tree is reassociated and all 32 rows are held at once
+        asm volatile("" : "+v"(z.x), "+v"(z.y), "+v"(z.z), "+v"(z.w));
+    }
+    return z;
+}
+
 #if defined(__HIP_DEVICE_COMPILE__)
 __device__ __forceinline__ uint32_t lds_u8(uint32_t addr) {
     return *(const __attribute__((address_space(3))) uint8_t*)(uintptr_t)addr;

@@ -9,6 +9,7 @@
 // kernels read record order[t] for thread t.
 #include <cstring>
 #include <rocprim/device/device_radix_sort.hpp>
+#include <rocprim/device/device_scan.hpp>
 #include <rocprim/iterator/counting_iterator.hpp>
 
 #include "common.h"
@@ -34,4 +35,95 @@ int tg_length_order(const uint32_t* len, uint64_t n, uint32_t* order, void* scra
         hipSuccess)
         return TG_EHIP;
     return TG_OK;
+}
+
+// ---- key-grouped octet jobs (key-table AES-GCM, aes_gcm_bs8.hip) ---------
+// The records of a key-table batch sorted by (key, length descending), then
+// cut into jobs of at most eight consecutive records of one key, so that a
+// wavefront runs a whole job with one key (its round keys and key planes
+// wave-uniform, one GHASH table per wave) and records of similar length.
+namespace {
+
+__global__ void kjp_keys(const uint32_t* __restrict__ key_idx, const uint32_t* __restrict__ len,
+                         uint32_t fixed_len, uint64_t n, uint64_t* __restrict__ ck) {
+    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= n) return;
+    const uint32_t L = len ? len[t] : fixed_len;
+    ck[t] = ((uint64_t)key_idx[t] << 32) | (uint64_t)(0xffffffffu - L);
+}
+
+__global__ void kjp_group_starts(const uint64_t* __restrict__ ck, uint64_t n, uint32_t* __restrict__ g) {
+    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= n) return;
+    g[t] = (t == 0 || (ck[t] >> 32) != (ck[t - 1] >> 32)) ? (uint32_t)t : 0u;
+}
+
+__global__ void kjp_job_starts(const uint32_t* __restrict__ gs, uint64_t n, uint32_t* __restrict__ js) {
+    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= n) return;
+    js[t] = (((uint32_t)t - gs[t]) & 7u) == 0 ? 1u : 0u;
+}
+
+__global__ void kjp_scatter(const uint32_t* __restrict__ js, const uint32_t* __restrict__ jx, uint64_t n,
+                            uint32_t* __restrict__ jobpos, uint32_t* __restrict__ njobs) {
+    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= n) return;
+    if (js[t]) jobpos[jx[t] - 1] = (uint32_t)t;
+    if (t == n - 1) {
+        *njobs = jx[t];
+        jobpos[jx[t]] = (uint32_t)n;
+    }
+}
+
+size_t ru256(size_t v) { return (v + 255) & ~(size_t)255; }
+
+}  // namespace
+
+// scratch == nullptr: *bytes = what a batch of n needs.  Outputs: order[n]
+// (record index per slot), jobpos[n + 1] (first slot of job j; jobpos[njobs]
+// = n), *njobs (device).  n < 2^32.
+int tg_key_job_plan(const uint32_t* key_idx, const uint32_t* len, uint32_t fixed_len, uint64_t n,
+                    uint32_t* order, uint32_t* jobpos, uint32_t* njobs, void* scratch, size_t* bytes,
+                    hipStream_t s) {
+    rocprim::counting_iterator<uint32_t> iota(0);
+    size_t t_sort = 0, t_max = 0, t_sum = 0;
+    if (rocprim::radix_sort_pairs(nullptr, t_sort, (uint64_t*)nullptr, (uint64_t*)nullptr, iota,
+                                  (uint32_t*)nullptr, (size_t)n, 0, 64, s) != hipSuccess ||
+        rocprim::inclusive_scan(nullptr, t_max, (uint32_t*)nullptr, (uint32_t*)nullptr, (size_t)n,
+                                rocprim::maximum<uint32_t>(), s) != hipSuccess ||
+        rocprim::inclusive_scan(nullptr, t_sum, (uint32_t*)nullptr, (uint32_t*)nullptr, (size_t)n,
+                                rocprim::plus<uint32_t>(), s) != hipSuccess)
+        return TG_EHIP;
+    const size_t b64 = ru256(n * 8), b32 = ru256(n * 4);
+    size_t tmp = t_sort > t_max ? t_sort : t_max;
+    tmp = tmp > t_sum ? tmp : t_sum;
+    const size_t need = 2 * b64 + 3 * b32 + ru256(tmp);
+    if (!scratch) {
+        *bytes = need;
+        return TG_OK;
+    }
+    if (*bytes < need || n == 0) return TG_EINVAL;
+    uint8_t* p = static_cast<uint8_t*>(scratch);
+    uint64_t* ck = reinterpret_cast<uint64_t*>(p);
+    uint64_t* ck_sorted = reinterpret_cast<uint64_t*>(p + b64);
+    uint32_t* g = reinterpret_cast<uint32_t*>(p + 2 * b64);
+    uint32_t* gs = reinterpret_cast<uint32_t*>(p + 2 * b64 + b32);
+    uint32_t* js = reinterpret_cast<uint32_t*>(p + 2 * b64 + 2 * b32);
+    void* t = p + 2 * b64 + 3 * b32;
+    const unsigned blocks = (unsigned)((n + 255) / 256);
+    hipLaunchKernelGGL(kjp_keys, dim3(blocks), dim3(256), 0, s, key_idx, len, fixed_len, n, ck);
+    size_t ts = t_sort;
+    if (rocprim::radix_sort_pairs(t, ts, ck, ck_sorted, iota, order, (size_t)n, 0, 64, s) != hipSuccess)
+        return TG_EHIP;
+    hipLaunchKernelGGL(kjp_group_starts, dim3(blocks), dim3(256), 0, s, ck_sorted, n, g);
+    size_t tm = t_max;
+    if (rocprim::inclusive_scan(t, tm, g, gs, (size_t)n, rocprim::maximum<uint32_t>(), s) != hipSuccess)
+        return TG_EHIP;
+    hipLaunchKernelGGL(kjp_job_starts, dim3(blocks), dim3(256), 0, s, gs, n, js);
+    uint32_t* jx = g;   // reused: the group starts are no longer needed
+    size_t tp = t_sum;
+    if (rocprim::inclusive_scan(t, tp, js, jx, (size_t)n, rocprim::plus<uint32_t>(), s) != hipSuccess)
+        return TG_EHIP;
+    hipLaunchKernelGGL(kjp_scatter, dim3(blocks), dim3(256), 0, s, js, jx, n, jobpos, njobs);
+    return hipGetLastError() == hipSuccess ? TG_OK : TG_EHIP;
 }

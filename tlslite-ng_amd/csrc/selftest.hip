@@ -19,7 +19,9 @@
 //      a multiple of 8 blocks, stride H^8 (gmul_rot tables of H^8), lift by
 //      H^(8 - l) (gf128_mul), XOR over the octet;
 //   5  the wave structure of gcm_wave_kernel (W = 1): front padding to a
-//      multiple of 64, stride H^64 (gmul tables of H^64), lift by H^(64 - l).
+//      multiple of 64, stride H^64 (gmul tables of H^64), lift by H^(64 - l);
+//   6  the octet structure of the key-table octet kernel (gcm_kt_kernel):
+//      stride H^8 through the wave's 4-bit tables (build_table4 / gmul4).
 #include <hip/hip_runtime.h>
 
 #include <cstring>
@@ -146,9 +148,11 @@ __global__ __launch_bounds__(256) void ghash_kernel(const uint8_t* hs, const uin
     const uint4 hw = load_partial(hs + 16 * i, 16);
     const uint4 hn = make_uint4(gcm_word_to_norm(hw.x), gcm_word_to_norm(hw.y), gcm_word_to_norm(hw.z),
                                 gcm_word_to_norm(hw.w));
-    constexpr uint32_t E = MODE == 4 ? 8 : MODE == 5 ? 64 : 1;
+    constexpr uint32_t E = (MODE == 4 || MODE == 6) ? 8 : MODE == 5 ? 64 : 1;
     const uint4 gn = E == 1 ? hn : gf128_pow(hn, E);           // G = H^E, normal order
-    if (MODE != 3) {
+    if (MODE == 6) {
+        if (threadIdx.x < 64) build_table4(0, gn);
+    } else if (MODE != 3) {
         const uint32_t gv[4] = {gcm_word_to_norm(gn.x), gcm_word_to_norm(gn.y), gcm_word_to_norm(gn.z),
                                 gcm_word_to_norm(gn.w)};
         const bool rot = MODE == 2 || MODE == 4;
@@ -188,14 +192,14 @@ __global__ __launch_bounds__(256) void ghash_kernel(const uint8_t* hs, const uin
     }
     // striped: S lanes, front padding to P = S ceil(M / S); lane l owns the
     // positions l, l + S, ... ; y <- y G ^ X (G = H^S), lifted by H^(S - l)
-    constexpr uint32_t S = MODE == 4 ? 8 : 64;
+    constexpr uint32_t S = (MODE == 4 || MODE == 6) ? 8 : 64;
     if (lane >= S) return;
     const uint32_t P = S * ((M + S - 1) / S), pad = P - M;
     uint4 y = make_uint4(0, 0, 0, 0);
     for (uint32_t t = lane; t < P; t += S) {
         if (t < pad) continue;   // leading zero blocks: y stays 0
         const uint4 x = gh_block(ad, alen, ct, clen, t - pad);
-        y = xor4(MODE == 4 ? gmul_rot(y, lane & 15u, kStJt) : gmul(y), x);
+        y = xor4(MODE == 4 ? gmul_rot(y, lane & 15u, kStJt) : MODE == 6 ? gmul4(y, 0) : gmul(y), x);
     }
     uint4 yn = norm4(y);
     if (yn.x | yn.y | yn.z | yn.w) yn = gf128_mul(yn, gf128_pow(hn, S - lane));
@@ -265,7 +269,7 @@ extern "C" __attribute__((visibility("default"))) int tg_selftest_poly1305(
 extern "C" __attribute__((visibility("default"))) int tg_selftest_ghash(
     int mode, const uint8_t* h, const uint8_t* aad, const uint64_t* aad_off, const uint32_t* aad_len,
     const uint8_t* ct, const uint64_t* ct_off, const uint32_t* ct_len, uint64_t n, uint8_t* out) {
-    if (!h || !aad_off || !aad_len || !ct_off || !ct_len || !out || mode < 0 || mode > 5 || n == 0 ||
+    if (!h || !aad_off || !aad_len || !ct_off || !ct_len || !out || mode < 0 || mode > 6 || n == 0 ||
         n > (1u << 16))
         return TG_EINVAL;
     DevBufs d;
@@ -293,7 +297,8 @@ extern "C" __attribute__((visibility("default"))) int tg_selftest_ghash(
         case 2: TG_ST_GHASH(2); break;
         case 3: TG_ST_GHASH(3); break;
         case 4: TG_ST_GHASH(4); break;
-        default: TG_ST_GHASH(5); break;
+        case 5: TG_ST_GHASH(5); break;
+        default: TG_ST_GHASH(6); break;
     }
 #undef TG_ST_GHASH
     if (hipGetLastError() != hipSuccess || hipDeviceSynchronize() != hipSuccess) return TG_EHIP;
