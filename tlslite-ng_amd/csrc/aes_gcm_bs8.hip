@@ -509,8 +509,9 @@ int launch_hy(const GcmKeyDev* key, const tg_batch& b, hipStream_t s, const uint
 // a key are consecutive, so a persistent wave would rarely keep its key, and
 // a loop around the job body made the compiler hoist its per-lane table and
 // plane addresses and spill ~180 VGPRs.  The grid is sized for the most jobs
-// a batch of n records can have (n / 8 rounded up per key: at most n); waves
-// past the planned count exit at once.
+// a batch of n records over nkeys keys can have (ceil(c_k / 8) per key k:
+// at most n / 8 + min(n, nkeys)); workgroups past the planned count exit at
+// once.
 constexpr int kKtThreads = 256;
 constexpr int kKtWaves = kKtThreads / 64;
 constexpr uint32_t kKtSbox = kKtWaves * 8192;            // after the per-wave tables
@@ -526,11 +527,13 @@ __global__ __launch_bounds__(kKtThreads, 4) void gcm_kt_kernel(const GcmTableKey
                                                             const uint32_t* __restrict__ order,
                                                             const uint32_t* __restrict__ jobpos,
                                                             const uint32_t* __restrict__ njobs_p) {
+    const uint32_t njobs = *njobs_p;
+    if (blockIdx.x * kKtWaves >= njobs) return;   // the whole workgroup (uniform)
     stage_sbox(kKtSbox);
     __syncthreads();
     const uint32_t wave = (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
     const uint32_t job = blockIdx.x * kKtWaves + wave;
-    if (job >= *njobs_p) return;
+    if (job >= njobs) return;
     const uint32_t tab = 8192u * wave, recw = kKtRecBase + wave * 1024u;
     const uint32_t p0 = gld(jobpos, job), p1 = gld(jobpos, job + 1);
     const uint32_t k = (uint32_t)__builtin_amdgcn_readfirstlane((int)gld(b.key_idx, gld(order, p0)));
@@ -551,8 +554,8 @@ __global__ void kt_planes_kernel(const GcmTableKey* __restrict__ keys, uint64_t 
 }
 
 template <int NR, bool OPEN>
-int launch_kt(const GcmTableKey* keys, const uint4* hpow, const uint32_t* planes, const tg_batch& b,
-              hipStream_t s) {
+int launch_kt(const GcmTableKey* keys, uint64_t nkeys, const uint4* hpow, const uint32_t* planes,
+              const tg_batch& b, hipStream_t s) {
     static bool attr_set = false;
     if (!attr_set) {
         if (hipFuncSetAttribute((const void*)gcm_kt_kernel<NR, OPEN>,
@@ -575,7 +578,8 @@ int launch_kt(const GcmTableKey* keys, const uint4* hpow, const uint32_t* planes
     rc = tg_key_job_plan(b.key_idx, b.len, b.fixed_len, b.n, order, jobpos, njobs, buf + so + sj + 256,
                          &plan, s);
     if (!rc) {
-        const uint64_t groups = (b.n + kKtWaves - 1) / kKtWaves;   // njobs <= n
+        const uint64_t maxjobs = (b.n + 7) / 8 + (nkeys < b.n ? nkeys : b.n);
+        const uint64_t groups = (maxjobs + kKtWaves - 1) / kKtWaves;
         hipLaunchKernelGGL((gcm_kt_kernel<NR, OPEN>), dim3((unsigned)groups), dim3(kKtThreads), kKtLds, s,
                            keys, hpow, planes, b, (const uint32_t*)order, (const uint32_t*)jobpos,
                            (const uint32_t*)njobs);
@@ -606,14 +610,14 @@ int tg_launch_gcm_bs8(const tg::GcmKeyDev* key, int rounds, const tg_batch& b, b
     return TG_EINVAL;
 }
 
-int tg_launch_gcm_kt(const tg::GcmTableKey* keys, const uint4* hpow, const uint32_t* planes, int rounds,
-                     const tg_batch& b, bool open, hipStream_t s) {
+int tg_launch_gcm_kt(const tg::GcmTableKey* keys, uint64_t nkeys, const uint4* hpow, const uint32_t* planes,
+                     int rounds, const tg_batch& b, bool open, hipStream_t s) {
     if (rounds == 10)
-        return open ? tg::launch_kt<10, true>(keys, hpow, planes, b, s)
-                    : tg::launch_kt<10, false>(keys, hpow, planes, b, s);
+        return open ? tg::launch_kt<10, true>(keys, nkeys, hpow, planes, b, s)
+                    : tg::launch_kt<10, false>(keys, nkeys, hpow, planes, b, s);
     if (rounds == 14)
-        return open ? tg::launch_kt<14, true>(keys, hpow, planes, b, s)
-                    : tg::launch_kt<14, false>(keys, hpow, planes, b, s);
+        return open ? tg::launch_kt<14, true>(keys, nkeys, hpow, planes, b, s)
+                    : tg::launch_kt<14, false>(keys, nkeys, hpow, planes, b, s);
     return TG_EINVAL;
 }
 

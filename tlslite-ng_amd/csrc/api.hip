@@ -175,7 +175,7 @@ int launch_kernels(tg_key* k, const tg_batch& b, bool open, hipStream_t s, const
         return tg_launch_ccm(static_cast<const tg::AesKeyDev*>(k->dev_key), k->nkeys > 1,
                              k->rounds, k->taglen, b, open, s);
     if (k->alg == TG_AES_GCM && k->nkeys > 1 && !order && kt_choice() == 14)
-        return tg_launch_gcm_kt(static_cast<const tg::GcmTableKey*>(k->dev_key), table_hpow(k),
+        return tg_launch_gcm_kt(static_cast<const tg::GcmTableKey*>(k->dev_key), k->nkeys, table_hpow(k),
                                 table_planes(k), k->rounds, b, open, s);
     if (k->alg == TG_AES_GCM && k->nkeys > 1)
         return tg_launch_gcm_table(static_cast<const tg::GcmTableKey*>(k->dev_key), table_hpow(k),

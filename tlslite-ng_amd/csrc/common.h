@@ -252,8 +252,8 @@ int tg_key_job_plan(const uint32_t* key_idx, const uint32_t* len, uint32_t fixed
                     hipStream_t s);
 // The key-table octet kernel (aes_gcm_bs8.hip): planes = per-key bitsliced
 // round-key planes (tg_launch_kt_planes), hpow = the keys' H^1..H^64.
-int tg_launch_gcm_kt(const tg::GcmTableKey* keys, const uint4* hpow, const uint32_t* planes, int rounds,
-                     const tg_batch& b, bool open, hipStream_t s);
+int tg_launch_gcm_kt(const tg::GcmTableKey* keys, uint64_t nkeys, const uint4* hpow, const uint32_t* planes,
+                     int rounds, const tg_batch& b, bool open, hipStream_t s);
 int tg_launch_kt_planes(const tg::GcmTableKey* keys, uint64_t n, int rounds, uint32_t* planes,
                         hipStream_t s);
 int tg_launch_ccm(const tg::AesKeyDev* keys, bool table, int rounds, int taglen,
