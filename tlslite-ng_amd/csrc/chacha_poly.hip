@@ -10,7 +10,8 @@
 //     four ciphertext blocks go straight into the Poly1305 accumulator, so
 //     mac_data = aad || pad || ct || pad || le64 || le64 (:60-63) is never
 //     materialised;
-//   * Poly1305 runs in five 26-bit limbs with 32x32->64 multiply-adds.
+//   * Poly1305 runs in 32-bit limbs with 32x32->64 multiply-adds (the wave
+//     kernel's striped Horner keeps five 26-bit limbs).
 #include <cstdlib>
 
 #include "common.h"
@@ -61,7 +62,7 @@ __device__ __forceinline__ void chacha_block(const uint32_t (&k)[8], uint32_t ct
 // ALIGNED records use 16-byte vector loads and stores with no branches.
 template <bool OPEN, bool ALIGNED>
 __device__ __forceinline__ void full_blocks(const uint32_t (&k)[8], uint4 nv, const uint8_t* in,
-                                            uint8_t* out, uint32_t j0, uint32_t nfull, Poly& p,
+                                            uint8_t* out, uint32_t j0, uint32_t nfull, Poly32& p,
                                             uint32_t (&ks)[16]) {
     if (j0 >= nfull) return;
     uint4 d[4];
@@ -125,7 +126,7 @@ __device__ __forceinline__ uint32_t swz(uint32_t r, uint32_t c) { return c ^ ((r
 template <bool OPEN>
 __device__ __forceinline__ void tiled_blocks(WaveTile& t, uint32_t lane, uint32_t nvalid,
                                              const uint32_t (&k)[8], uint4 nv, uint32_t jmin,
-                                             Poly& p, uint32_t (&ks)[16]) {
+                                             Poly32& p, uint32_t (&ks)[16]) {
     const uint32_t grp = lane >> 5, cq = lane & 7u, rq = lane >> 3;
     // the coalesced ops of group g's pair starting at block p0 (even)
     auto load_pair = [&](uint32_t g, uint32_t p0, uint4 (&R)[4]) {
@@ -224,7 +225,7 @@ __global__ __launch_bounds__(kChachaThreads, MINW) void chacha_kernel(
     const bool aligned = (((uintptr_t)in | (uintptr_t)out) & 15) == 0;
     const uint4 nv = load_partial(b.nonce + 12 * i, 12);
 
-    Poly p;
+    Poly32 p;   // radix 2^32 (poly1305.h)
     {
         uint32_t otk[16];
         chacha_block(k, 0, nv.x, nv.y, nv.z, otk);  // poly1305_key_gen

@@ -95,6 +95,94 @@ __device__ __forceinline__ uint4 poly_finish(const Poly& p) {
     return make_uint4(w0, w1, w2, w3);
 }
 
+// ---- radix 2^32 (the lane-per-record kernel) ------------------------------
+// h = h0 + h1 2^32 + h2 2^64 + h3 2^96 + h4 2^128 with h0..h3 full words and
+// h4 a few bits.  The clamp leaves r0 < 2^28 and r1..r3 < 2^28, multiples of
+// 4, so a product term at or above 2^128 folds through 2^130 == 5 as
+// h_i * s_j with s_j = r_j + r_j / 4 = 5 r_j / 4 (exact): every column is a
+// sum of at most five products < 2^60.4, no 64-bit overflow.  Per 16 bytes:
+// 19 v_mad_u64_u32 and one 32-bit multiply, no limb splitting of the message
+// (the 26-bit form takes 25 multiply-adds plus the splits and 26-bit
+// carries).
+struct Poly32 {
+    uint32_t r0, r1, r2, r3;
+    uint32_t s1, s2, s3;
+    uint32_t h0, h1, h2, h3, h4;
+    uint32_t p0, p1, p2, p3;  // s half of the one-time key
+};
+
+__device__ __forceinline__ void poly_init(Poly32& p, const uint32_t (&otk)[16]) {
+    // r = LE(key[0:16]) & 0x0ffffffc0ffffffc0ffffffc0fffffff (poly1305.py:37-38)
+    p.r0 = otk[0] & 0x0fffffffu;
+    p.r1 = otk[1] & 0x0ffffffcu;
+    p.r2 = otk[2] & 0x0ffffffcu;
+    p.r3 = otk[3] & 0x0ffffffcu;
+    p.s1 = p.r1 + (p.r1 >> 2);
+    p.s2 = p.r2 + (p.r2 >> 2);
+    p.s3 = p.r3 + (p.r3 >> 2);
+    p.h0 = p.h1 = p.h2 = p.h3 = p.h4 = 0;
+    p.p0 = otk[4]; p.p1 = otk[5]; p.p2 = otk[6]; p.p3 = otk[7];
+}
+
+// acc = (acc + LE(m) + hib 2^128) * r mod 2^130 - 5 (poly1305.py:43-46);
+// hib = 1 for a full block, 0 for a raw message's short last block (its 0x01
+// already inside m).
+__device__ __forceinline__ void poly_block(Poly32& p, uint4 m, uint32_t hib = 1u) {
+    uint64_t t = (uint64_t)p.h0 + m.x;
+    const uint32_t h0 = (uint32_t)t;
+    t = (uint64_t)p.h1 + m.y + (t >> 32);
+    const uint32_t h1 = (uint32_t)t;
+    t = (uint64_t)p.h2 + m.z + (t >> 32);
+    const uint32_t h2 = (uint32_t)t;
+    t = (uint64_t)p.h3 + m.w + (t >> 32);
+    const uint32_t h3 = (uint32_t)t;
+    const uint32_t h4 = p.h4 + hib + (uint32_t)(t >> 32);
+    const uint64_t d0 = mul64(h0, p.r0) + mul64(h1, p.s3) + mul64(h2, p.s2) + mul64(h3, p.s1);
+    uint64_t d1 = mul64(h0, p.r1) + mul64(h1, p.r0) + mul64(h2, p.s3) + mul64(h3, p.s2) + mul64(h4, p.s1);
+    uint64_t d2 = mul64(h0, p.r2) + mul64(h1, p.r1) + mul64(h2, p.r0) + mul64(h3, p.s3) + mul64(h4, p.s2);
+    uint64_t d3 = mul64(h0, p.r3) + mul64(h1, p.r2) + mul64(h2, p.r1) + mul64(h3, p.r0) + mul64(h4, p.s3);
+    d1 += d0 >> 32;
+    d2 += d1 >> 32;
+    d3 += d2 >> 32;
+    // bits 128.. : h4 r0 plus the carry out of d3 (< 2^31 + 2^31)
+    const uint32_t d4 = h4 * p.r0 + (uint32_t)(d3 >> 32);
+    // fold 2^130 * (d4 >> 2) as 5 (d4 >> 2) = (d4 >> 2) + (d4 & ~3)
+    t = (uint64_t)(uint32_t)d0 + (d4 >> 2) + (d4 & ~3u);
+    p.h0 = (uint32_t)t;
+    t = (uint64_t)(uint32_t)d1 + (t >> 32);
+    p.h1 = (uint32_t)t;
+    t = (uint64_t)(uint32_t)d2 + (t >> 32);
+    p.h2 = (uint32_t)t;
+    t = (uint64_t)(uint32_t)d3 + (t >> 32);
+    p.h3 = (uint32_t)t;
+    p.h4 = (d4 & 3u) + (uint32_t)(t >> 32);
+}
+
+// tag = LE16((acc + s) mod 2^128) (poly1305.py:47-48).  h < 5 * 2^128 < 2p,
+// so one conditional subtraction of p gives acc mod p.
+__device__ __forceinline__ uint4 poly_finish(const Poly32& p) {
+    uint64_t t = (uint64_t)p.h0 + 5;
+    const uint32_t g0 = (uint32_t)t;
+    t = (uint64_t)p.h1 + (t >> 32);
+    const uint32_t g1 = (uint32_t)t;
+    t = (uint64_t)p.h2 + (t >> 32);
+    const uint32_t g2 = (uint32_t)t;
+    t = (uint64_t)p.h3 + (t >> 32);
+    const uint32_t g3 = (uint32_t)t;
+    const uint32_t g4 = p.h4 + (uint32_t)(t >> 32);
+    const uint32_t sel = 0u - (g4 >> 2);   // all ones when h + 5 >= 2^130, i.e. h >= p
+    const uint32_t w0 = (p.h0 & ~sel) | (g0 & sel), w1 = (p.h1 & ~sel) | (g1 & sel);
+    const uint32_t w2 = (p.h2 & ~sel) | (g2 & sel), w3 = (p.h3 & ~sel) | (g3 & sel);
+    t = (uint64_t)w0 + p.p0;
+    const uint32_t o0 = (uint32_t)t;
+    t = (uint64_t)w1 + p.p1 + (t >> 32);
+    const uint32_t o1 = (uint32_t)t;
+    t = (uint64_t)w2 + p.p2 + (t >> 32);
+    const uint32_t o2 = (uint32_t)t;
+    t = (uint64_t)w3 + p.p3 + (t >> 32);
+    return make_uint4(o0, o1, o2, (uint32_t)t);
+}
+
 struct F5 {
     uint32_t h0, h1, h2, h3, h4;
 };

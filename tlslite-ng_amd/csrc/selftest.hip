@@ -6,7 +6,7 @@
 // record path.
 //
 // Poly1305 modes (poly1305.h):
-//   0  lane Horner, as chacha_kernel (one message per lane);
+//   0  lane Horner in radix 2^32 (Poly32), as chacha_kernel (one message per lane);
 //   1  wave-striped Horner with the r^(4S-4) gaps, the lift and the shuffle
 //      sum of chacha_wave_kernel, W = 1 (S = 64 threads per message);
 //   2  the same with W = 4;  3  W = 16.
@@ -65,14 +65,14 @@ __global__ void poly_lane_kernel(const uint8_t* keys, const uint8_t* msgs, const
     const uint4 k0 = load_partial(keys + 32 * i, 16), k1 = load_partial(keys + 32 * i + 16, 16);
     otk[0] = k0.x; otk[1] = k0.y; otk[2] = k0.z; otk[3] = k0.w;
     otk[4] = k1.x; otk[5] = k1.y; otk[6] = k1.z; otk[7] = k1.w;
-    Poly p;
+    Poly32 p;   // as chacha_kernel
     poly_init(p, otk);
     const uint8_t* m = msgs + off[i];
     const uint32_t nb = (len[i] + 15) >> 4;
     for (uint32_t k = 0; k < nb; ++k) {
         uint32_t hib;
         const uint4 blk = msg_block(m, len[i], k, true, hib);
-        poly_block(p, blk, hib);
+        poly_block(p, blk, hib ? 1u : 0u);   // radix 2^32: the 2^128 bit is 1 in h4
     }
     store_partial(tags + 16 * i, poly_finish(p), 16);
 }

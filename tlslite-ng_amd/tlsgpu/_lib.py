@@ -99,10 +99,13 @@ def load():
     global _lib
     if _lib is not None:
         return _lib
-    if not os.path.exists(LIB_PATH):
+    # TLSGPU_LIB: an alternative build of the same library (A/B kernel
+    # measurements in tools/, never set by the package itself)
+    path = os.environ.get("TLSGPU_LIB") or LIB_PATH
+    if not os.path.exists(path):
         raise OSError("libtlsgpu.so not built (run __graft_entry__.build() or "
-                      "make -C tlslite-ng_amd/csrc): %s" % LIB_PATH)
-    l = ctypes.CDLL(LIB_PATH)
+                      "make -C tlslite-ng_amd/csrc): %s" % path)
+    l = ctypes.CDLL(path)
     p, sz, i, u64 = ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int, ctypes.c_uint64
     l.tg_version.restype = ctypes.c_char_p
     l.tg_version.argtypes = []
