@@ -130,6 +130,13 @@ struct SingleKeyCtx {   // one key for the batch: 8-bit H^8 tables in LDS (gmul_
     __device__ __forceinline__ uint4 hpow(int e) const { return key->hpow[e - 1]; }
     __device__ __forceinline__ uint4 gmul(uint4 y) const { return gmul_rot(y, threadIdx.x & 15u, jt); }
 };
+struct SingleKeyRowCtx {   // SingleKeyCtx with the lane's offset row held in registers
+    const GcmKeyDev* key;
+    uint4 jw;
+    __device__ __forceinline__ const uint32_t* rk() const { return key->rk; }
+    __device__ __forceinline__ uint4 hpow(int e) const { return key->hpow[e - 1]; }
+    __device__ __forceinline__ uint4 gmul(uint4 y) const { return gmul_rot_j(y, threadIdx.x & 15u, jw); }
+};
 struct TableKeyCtx {    // a key of a key table: the wave's 4-bit H^8 tables in LDS (gmul4)
     const uint32_t* rkw;
     const uint4* hp;    // H^1 .. H^64 of this key (tg_launch_table_hpow)
@@ -382,6 +389,7 @@ __global__ __launch_bounds__(kHyThreads) void gcm_hy_kernel(const GcmKeyDev* __r
     const uint32_t wave = (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
     const uint64_t njobs = (bp->n + 7) / 8;
     const uint32_t recw = kHyRecBase + wave * 1024u;
+    const uint4 jw = lds_u128(kHyJt + ((threadIdx.x & 15u) << 4));
     if (wave < nt) {
         if (prio) __builtin_amdgcn_s_setprio(1);
         const RkLds rk{kHyRk};
@@ -392,7 +400,7 @@ __global__ __launch_bounds__(kHyThreads) void gcm_hy_kernel(const GcmKeyDev* __r
             if (job >= njobs) break;
             asm volatile("" ::: "memory");
             const tg_batch b = *bp;
-            octet_job<NR, OPEN, true>(SingleKeyCtx{key, kHyJt}, b, order, 8ull * job, recw, rk,
+            octet_job<NR, OPEN, true>(SingleKeyRowCtx{key, jw}, b, order, 8ull * job, recw, rk,
                                       kHySbox, bs8::KeyPlanesLds{kHyKeys});
         }
     } else {

@@ -73,8 +73,7 @@ __device__ __forceinline__ uint4 gmul_lowreg(uint4 y) {
 // of lane l come from a 16-row LDS table at ``jt`` (row l % 16: byte k of word
 // q = ((l + 4 q + k) % 16) * 16).  lane16 = l % 16.  At most eight table rows
 // in flight (32 VGPRs).
-__device__ __forceinline__ uint4 gmul_rot(uint4 y, uint32_t lane16, uint32_t jt) {
-    const uint4 jw = lds_u128(jt + (lane16 << 4));
+__device__ __forceinline__ uint4 gmul_rot_j(uint4 y, uint32_t lane16, uint4 jw) {
     uint32_t u0 = y.x, u1 = y.y, u2 = y.z, u3 = y.w;
     if (lane16 & 8u) { uint32_t t = u0; u0 = u2; u2 = t; t = u1; u1 = u3; u3 = t; }
     if (lane16 & 4u) { uint32_t t = u0; u0 = u1; u1 = u2; u2 = u3; u3 = t; }
@@ -98,6 +97,11 @@ __device__ __forceinline__ uint4 gmul_rot(uint4 y, uint32_t lane16, uint32_t jt)
         z = xor4_3(z, e[6], e[7]);
     }
     return z;
+}
+
+// gmul_rot with the lane-offset row read from LDS per multiply.
+__device__ __forceinline__ uint4 gmul_rot(uint4 y, uint32_t lane16, uint32_t jt) {
+    return gmul_rot_j(y, lane16, lds_u128(jt + (lane16 << 4)));
 }
 
 // Stage the 8-bit tables of ``src`` (GcmKeyDev layout, entry (j, b) at
