@@ -1,0 +1,13 @@
+# Build an alternative libtlsgpu.so for A/B runs (TLSGPU_LIB=...): object
+# NAME.hip recompiled with extra flags, linked with the tree's other objects.
+# usage: bash tools/build_variant.sh NAME OUT.so -DFLAG ...
+set -e
+R=$(cd "$(dirname "$0")/.." && pwd)
+C=$R/tlslite-ng_amd/csrc
+NAME=$1; OUT=$2; shift 2
+T=$(mktemp -d)
+/opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -I$R/include -I$C -Wall -Wno-unused-result \
+  -fvisibility=hidden "$@" -c -o $T/$NAME.o $C/$NAME.hip
+OBJS=$(ls $C/obj/*.o | grep -v "/$NAME.o$")
+/opt/rocm/bin/hipcc -shared -fPIC --offload-arch=gfx950 -o $OUT $T/$NAME.o $OBJS
+rm -rf $T
