@@ -48,7 +48,18 @@ static uint32_t le(const uint8_t* p) {
     return p[0] | p[1] << 8 | p[2] << 16 | (uint32_t)p[3] << 24;
 }
 
-template <int NR>
+// The folded planes (keymath.h bs8_fold_word) in bs8mask order, read as rows:
+// encrypt() then runs mix_round_folded (the device's KeyPlanesVmemFolded).
+struct FoldedRows {
+    static constexpr bool kFolded = true;
+    const uint32_t* w;
+    tg::bs8::Word4 row4(int r, int b) const {
+        return tg::bs8::word4(w[(4 * r) * 8 + b], w[(4 * r + 1) * 8 + b], w[(4 * r + 2) * 8 + b],
+                              w[(4 * r + 3) * 8 + b]);
+    }
+};
+
+template <int NR, bool FOLD>
 static int run(int klen, unsigned seed) {
     srand(seed);
     uint8_t key[32], rk[16 * 15], nonce[12];
@@ -59,7 +70,11 @@ static int run(int klen, unsigned seed) {
     for (int q = 0; q < 4 * (NR + 1); ++q) rkw[q] = le(rk + 4 * q);
     uint32_t planes[15 * 32];
     for (int e = 0; e < 32 * (NR + 1); ++e) planes[e] = tg::bs8::mask_word(rkw, e);
+    uint32_t folded[15 * 32];
+    for (int e = 0; e < 32 * (NR + 1); ++e)
+        folded[e] = (e >> 5) >= 1 && (e >> 5) < NR ? tg::bs8_fold_word(rkw, e) : planes[e];
     const tg::bs8::KeyPlanes km{planes};
+    const FoldedRows kf{folded};
     const uint32_t u[4] = {le(nonce) ^ rkw[0], le(nonce + 4) ^ rkw[1], le(nonce + 8) ^ rkw[2], rkw[3]};
     int bad = 0, checked = 0;
     const uint32_t betas[] = {0, 1, 2, 3, 7, 15, 16, 255, 256, 1022, 1023, 1024, 1025,
@@ -74,7 +89,10 @@ static int run(int klen, unsigned seed) {
             for (int b = 0; b < 6; ++b) s[3][b] ^= lane[b];
             tg::bs8::ctr_planes<6, 16>(s, kmask, beta);
             if ((beta + 1u) >> 10) tg::bs8::ctr_planes<16, 32>(s, kmask, beta);
-            tg::bs8::encrypt<NR>(s, km, w);
+            if (FOLD)
+                tg::bs8::encrypt<NR>(s, kf, w);
+            else
+                tg::bs8::encrypt<NR>(s, km, w);
             for (int j = 0; j < 8; ++j) {
                 const uint32_t ctr = c0 + 64u * beta + 8u * j;
                 uint8_t blk[16], want[16];
@@ -95,7 +113,7 @@ static int run(int klen, unsigned seed) {
             }
         }
     }
-    printf("NR=%d seed=%u blocks=%d bad=%d\n", NR, seed, checked, bad);
+    printf("NR=%d fold=%d seed=%u blocks=%d bad=%d\n", NR, (int)FOLD, seed, checked, bad);
     return bad;
 }
 
@@ -103,8 +121,10 @@ int main() {
     make_sbox();
     int bad = 0;
     for (unsigned seed = 1; seed <= 4; ++seed) {
-        bad += run<10>(16, seed);
-        bad += run<14>(32, 100 + seed);
+        bad += run<10, false>(16, seed);
+        bad += run<14, false>(32, 100 + seed);
+        bad += run<10, true>(16, seed);
+        bad += run<14, true>(32, 100 + seed);
     }
     // the per-record plane of a lane equals the plain bit test (GcmKeyDev::bs8mask layout)
     printf(bad ? "FAIL\n" : "OK\n");

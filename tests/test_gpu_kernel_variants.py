@@ -72,7 +72,7 @@ def test_forced_kernel_vs_oracle(torch, tg, oracle_mod, alg, klen, var, value, a
                       tamper=(1, 30, 111))
 
 
-@pytest.mark.parametrize("keys", ["0", "2"])          # key planes from LDS / vector loads
+@pytest.mark.parametrize("keys", ["0", "1", "2"])   # LDS / scalar loads / row layout (default 4: folded)
 @pytest.mark.parametrize("klen", [16, 32])
 def test_hybrid_key_plane_sources(torch, tg, oracle_mod, keys, klen, monkeypatch):
     """The hybrid kernel's alternative key-plane providers (TLSGPU_HY_KEYS)."""

@@ -59,6 +59,7 @@ TG_BS_HD Word4 word4(uint32_t a, uint32_t b, uint32_t c, uint32_t d) { return Wo
 
 // Key-plane providers: row4(r, b) = the planes (r, i, b) of rows i = 0..3.
 struct KeyPlanes {   // key planes in memory (host: plain reads; device: scalar loads)
+    static constexpr bool kFolded = false;
     const uint32_t* w;
     TG_BS_MF uint32_t operator()(int r, int i, int b) const {
 #if defined(__HIP_DEVICE_COMPILE__)
@@ -78,6 +79,7 @@ struct KeyPlanes {   // key planes in memory (host: plain reads; device: scalar 
 // profiles/r02/v5_issue_probe2.txt).  stage_lds_planes writes the layout.
 #if defined(__HIPCC__)
 struct KeyPlanesLds {
+    static constexpr bool kFolded = false;
     uint32_t base;
     __device__ __forceinline__ uint4 row4(int r, int b) const {
 #if defined(__HIP_DEVICE_COMPILE__)
@@ -93,6 +95,7 @@ struct KeyPlanesLds {
 // which the octet kernels barely use, so neither the VALU (SGPR operands) nor
 // the LDS (the T-table waves' pipe) pays for the key planes.
 struct KeyPlanesVmem {
+    static constexpr bool kFolded = false;
     const uint4* rows;
     __device__ __forceinline__ uint4 row4(int r, int b) const {
 #if defined(__HIP_DEVICE_COMPILE__)
@@ -103,6 +106,16 @@ struct KeyPlanesVmem {
         return rows[8 * r + b];
 #endif
     }
+};
+
+// The same row layout holding the folded planes (keymath.h bs8_fold_word) of
+// rounds 1 .. NR - 1: encrypt() runs mix_round_folded.  The rows' addresses
+// are wave-uniform, so the compiler reads them with s_load_dwordx16 (both
+// providers): the folded gates take SGPR operands and still win, 20 gates
+// per round fewer (profiles/r02/v58_fold_keys/; from LDS, VGPR operands,
+// they measured no better).
+struct KeyPlanesVmemFolded : KeyPlanesVmem {
+    static constexpr bool kFolded = true;
 };
 
 // Plane (r, i, b) of the (NR + 1) * 32 in ``src`` (GcmKeyDev::bs8mask order)
@@ -201,6 +214,50 @@ TG_BS_HD void mix_round(uint32_t (*s)[8], const KM& km, int r) {
     }
 }
 
+// mix_round with the round key folded into the column XORs: with the planes
+// c of bs8_fold_word (x c_i ^ c_(i+2) = k_i), T_i = a_i ^ a_(i+1) ^ c_i is one
+// 3-input gate and out_i = x T_i ^ a_(i+1) ^ T_(i+2) already carries k_i, so
+// the five planes without xtime feedback take one gate per row instead of
+// two (20 gates per round fewer).  Provider: KeyPlanesVmemFolded (the
+// hybrid kernel's default).
+template <class KM>
+TG_BS_HD void mix_round_folded(uint32_t (*s)[8], const KM& km, int r) {
+    uint32_t a7[4], T7[4], Tp[4];
+    const Word4 c7 = km.row4(r, 7);
+    const uint32_t c7w[4] = {c7.x, c7.y, c7.z, c7.w};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) a7[i] = rotr_bytes(s[i][7], i);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) T7[i] = xor3(a7[i], a7[(i + 1) & 3], c7w[i]);
+    TG_BS8_FENCE();
+#pragma unroll
+    for (int b = 0; b < 8; ++b) {
+        uint32_t a[4], T[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) a[i] = b == 7 ? a7[i] : rotr_bytes(s[i][b], i);
+        if (b == 7) {
+#pragma unroll
+            for (int i = 0; i < 4; ++i) T[i] = T7[i];
+        } else {
+            const Word4 c4 = km.row4(r, b);
+            const uint32_t cw[4] = {c4.x, c4.y, c4.z, c4.w};
+#pragma unroll
+            for (int i = 0; i < 4; ++i) T[i] = xor3(a[i], a[(i + 1) & 3], cw[i]);
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const uint32_t Tprev = b == 0 ? T7[i] : Tp[i];
+            if (b == 1 || b == 3 || b == 4)
+                s[i][b] = xor3(Tprev, T7[i], a[(i + 1) & 3]) ^ T[(i + 2) & 3];
+            else
+                s[i][b] = xor3(Tprev, a[(i + 1) & 3], T[(i + 2) & 3]);
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) Tp[i] = T[i];
+        TG_BS8_FENCE();
+    }
+}
+
 // 8 x 8 bit transpose inside every byte of a[0..7]: bit j of byte c of a[b]
 // <-> bit b of byte c of a[j] (three swap stages, two shifts + two bitop3
 // per pair).
@@ -259,7 +316,10 @@ TG_BS_HD void encrypt(uint32_t (*s)[8], const KM& km, uint32_t (*w)[8]) {
             bs::sbox(s[i]);
             TG_BS8_FENCE();
         }
-        mix_round(s, km, r);
+        if constexpr (KM::kFolded)
+            mix_round_folded(s, km, r);
+        else
+            mix_round(s, km, r);
     }
 #pragma unroll
     for (int i = 0; i < 4; ++i) {

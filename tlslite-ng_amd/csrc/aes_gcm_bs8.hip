@@ -418,6 +418,9 @@ __global__ __launch_bounds__(kHyThreads) void gcm_hy_kernel(const GcmKeyDev* __r
             else if (KEYS == 2)
                 octet_job<NR, OPEN, false>(SingleKeyCtx{key, kHyJt}, b, order, 8ull * job, recw,
                                            none, kHySbox, bs8::KeyPlanesVmem{krows});
+            else if (KEYS == 4)
+                octet_job<NR, OPEN, false>(SingleKeyCtx{key, kHyJt}, b, order, 8ull * job, recw,
+                                           none, kHySbox, bs8::KeyPlanesVmemFolded{{krows}});
             else
                 octet_job<NR, OPEN, false>(SingleKeyCtx{key, kHyJt}, b, order, 8ull * job, recw,
                                            none, kHySbox, bs8::KeyPlanes{key->bs8mask});
@@ -427,15 +430,18 @@ __global__ __launch_bounds__(kHyThreads) void gcm_hy_kernel(const GcmKeyDev* __r
 
 // Stream-ordered setup of the hybrid kernel's scratch: the job counter and a
 // device copy of the batch descriptor.
+// fold: the rows hold bs8_fold_word planes (KeyPlanesVmemFolded) for rounds
+// 1 .. nr - 1 instead of the round-key planes.
 __global__ void hy_setup_kernel(tg_batch b, uint32_t* queue, tg_batch* bcopy,
-                                const GcmKeyDev* __restrict__ key, uint32_t* krows, int nr) {
+                                const GcmKeyDev* __restrict__ key, uint32_t* krows, int nr, int fold) {
     if (threadIdx.x == 0) {
         *queue = 0;
         *bcopy = b;
     }
     for (int e = threadIdx.x; e < 32 * (nr + 1); e += blockDim.x) {   // KeyPlanesVmem layout
         const int r = e >> 5, i = (e >> 3) & 3, bit = e & 7;
-        krows[4 * (8 * r + bit) + i] = key->bs8mask[e];
+        krows[4 * (8 * r + bit) + i] =
+            fold && r >= 1 && r < nr ? bs8_fold_word(key->rk, e) : key->bs8mask[e];
     }
 }
 
@@ -472,7 +478,8 @@ int launch_hy_k(const GcmKeyDev* key, const tg_batch& b, hipStream_t s, const ui
     uint32_t* queue = reinterpret_cast<uint32_t*>(scratch);
     tg_batch* bcopy = reinterpret_cast<tg_batch*>(scratch + 64);
     uint32_t* krows = reinterpret_cast<uint32_t*>(scratch + 256);
-    hipLaunchKernelGGL(hy_setup_kernel, dim3(1), dim3(64), 0, s, b, queue, bcopy, key, krows, NR);
+    hipLaunchKernelGGL(hy_setup_kernel, dim3(1), dim3(64), 0, s, b, queue, bcopy, key, krows, NR,
+                       KEYS == 4 ? 1 : 0);
     bool ok = hipGetLastError() == hipSuccess;
     if (ok) {
         hipLaunchKernelGGL((gcm_hy_kernel<NR, OPEN, KEYS>), dim3((unsigned)device_cus()), dim3(kHyThreads),
@@ -485,9 +492,11 @@ int launch_hy_k(const GcmKeyDev* key, const tg_batch& b, hipStream_t s, const ui
 }
 
 // TLSGPU_HY_T (T-table waves per 16, default 8), TLSGPU_HY_PRIO (default 1)
-// and TLSGPU_HY_KEYS (1: key planes by scalar loads, default; 0: from LDS,
-// 2 % slower in the hybrid: the T-table waves own the LDS,
-// profiles/r02/v25_hy_keys.txt) are read per launch (measurement).
+// and TLSGPU_HY_KEYS (4: the MixColumns-folded planes by scalar loads,
+// default, 1.3 % faster than 1, profiles/r02/v58_fold_keys/; 1: the round-key
+// planes by scalar loads; 0: from LDS, 2 % slower than 1 in the hybrid: the
+// T-table waves own the LDS, profiles/r02/v25_hy_keys.txt; 2: the row layout
+// by (compiler-scalarised) loads) are read per launch (measurement).
 template <int NR, bool OPEN>
 int launch_hy(const GcmKeyDev* key, const tg_batch& b, hipStream_t s, const uint32_t* order) {
     if ((b.n + 7) / 8 > 0xffffffffull) return TG_EINVAL;
@@ -496,9 +505,10 @@ int launch_hy(const GcmKeyDev* key, const tg_batch& b, hipStream_t s, const uint
     const char* ek = getenv("TLSGPU_HY_KEYS");
     const uint32_t nt = et ? (uint32_t)atoi(et) : 8u;
     const uint32_t prio = ep ? (uint32_t)atoi(ep) : 1u;
-    const int keys = ek ? atoi(ek) : 1;
+    const int keys = ek ? atoi(ek) : 4;
     if (keys == 0) return launch_hy_k<NR, OPEN, 0>(key, b, s, order, nt, prio);
     if (keys == 2) return launch_hy_k<NR, OPEN, 2>(key, b, s, order, nt, prio);
+    if (keys == 4) return launch_hy_k<NR, OPEN, 4>(key, b, s, order, nt, prio);
     return launch_hy_k<NR, OPEN, 1>(key, b, s, order, nt, prio);
 }
 

@@ -87,4 +87,34 @@ TG_KM_HD uint32_t bs8_mask_word(const uint32_t* rk, int e) {
     return m;
 }
 
+// The MixColumns-folded round-key planes (aes_bs8.h mix_round_folded), entry
+// e = (4 r + i) * 8 + b for r >= 1: byte c is 0xff iff bit b of c_i is set,
+// where per column c (k_i = byte i of rk[4 r + c] ^ 0x63636363, x = 0x02)
+//   c_0 = (k_2 ^ x k_0) / (1 ^ x^2),  c_2 = k_0 ^ x c_0,
+//   c_1 = (k_3 ^ x k_1) / (1 ^ x^2),  c_3 = k_1 ^ x c_1,
+// so that x c_i ^ c_(i+2) = k_i: MixColumns of T_i = t_i ^ c_i adds the round key
+// (1 / (1 ^ x^2) = 0x52 in GF(2^8) mod 0x11b).
+TG_KM_HD uint32_t gf8_mul(uint32_t a, uint32_t b) {
+    uint32_t r = 0;
+    for (int k = 0; k < 8; ++k) {
+        if ((b >> k) & 1u) r ^= a;
+        a = (a << 1) ^ ((a & 0x80u) ? 0x11bu : 0u);
+    }
+    return r & 0xffu;
+}
+
+TG_KM_HD uint32_t bs8_fold_word(const uint32_t* rk, int e) {
+    const int r = e >> 5, i = (e >> 3) & 3, b = e & 7;
+    uint32_t m = 0;
+    for (int c = 0; c < 4; ++c) {
+        const uint32_t w = rk[4 * r + c] ^ 0x63636363u;
+        const uint32_t lo = i & 1;   // rows lo and lo + 2 form one system
+        const uint32_t k0 = (w >> (8 * lo)) & 0xffu, k2 = (w >> (8 * (lo + 2))) & 0xffu;
+        const uint32_t cl = gf8_mul(k2 ^ gf8_mul(k0, 2), 0x52);
+        const uint32_t ci = i < 2 ? cl : k0 ^ gf8_mul(cl, 2);
+        if ((ci >> b) & 1u) m |= 0xffu << (8 * c);
+    }
+    return m;
+}
+
 }  // namespace tg
