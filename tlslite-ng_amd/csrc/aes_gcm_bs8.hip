@@ -194,7 +194,8 @@ __device__ __forceinline__ void octet_job(const KC& kc, const tg_batch& b,
     const uint32_t nfl = nfull > rho ? (nfull - rho + 7u) >> 3 : 0u;    // full ones
     const uint32_t nbatch = wave_max_u32((nvl + 7u) >> 3);
     // batches in which every valid lane of the wave has all eight blocks full
-    const uint32_t nfast = __all(!valid || aligned) ? wave_min_u32(valid ? nfl >> 3 : 0xffffffffu) : 0u;
+    // (any alignment: the fast path's accesses are gload16u / gstore16u)
+    const uint32_t nfast = wave_min_u32(valid ? nfl >> 3 : 0xffffffffu);
 
     // GHASH over this lane's AAD positions (aesgcm.py:69-79), zero-padded blocks
     uint4 y = make_uint4(0, 0, 0, 0);
@@ -216,13 +217,13 @@ __device__ __forceinline__ void octet_job(const KC& kc, const tg_batch& b,
                 uint4 d[N];
 #pragma unroll
                 for (int q = 0; q < N; ++q)
-                    d[q] = gload16(in + 16u * (blk0 + 8u * (j0 + q)));
+                    d[q] = gload16u(in + 16u * (blk0 + 8u * (j0 + q)));
 #pragma unroll
                 for (int q = 0; q < N; ++q) {
                     const uint4 k = ks[q];
                     const uint4 c = make_uint4(xor3(d[q].x, k.x, rkl.x), xor3(d[q].y, k.y, rkl.y),
                                                xor3(d[q].z, k.z, rkl.z), xor3(d[q].w, k.w, rkl.w));
-                    gstore16(out + 16u * (blk0 + 8u * (j0 + q)), c);
+                    gstore16u(out + 16u * (blk0 + 8u * (j0 + q)), c);
                     if (!OPEN) d[q] = c;
                 }
 #pragma unroll
@@ -252,6 +253,13 @@ __device__ __forceinline__ void octet_job(const KC& kc, const tg_batch& b,
     for (uint32_t beta = 0; beta < nbatch; ++beta) {
         const uint32_t blk0 = rho + 64u * beta;   // block of slot j: blk0 + 8 j
         const uint32_t c0 = 2u + blk0;             // its counter: c0 + 8 j
+        // A batch in which no lane has more than one (four) of its blocks
+        // left -- the last one of a record of 64 q + 1 blocks, e.g. a full TLS
+        // 1.3 record's 16 385-byte inner plaintext -- runs one block per lane
+        // (one T-table half) instead of eight (two).  Seal only on the
+        // bitsliced waves: in the open kernel the extra path's registers
+        // spill elsewhere and cost 2 % (profiles/r02/v66_one_block/).
+        const bool one = !OPEN && __all(!valid || nvl <= 8u * beta + 1u);
         if (TROLE) {
             // through the 256-counter window cache when no lane of the wave
             // crosses a window in this batch (wave-uniform); two halves of four
@@ -260,11 +268,18 @@ __device__ __forceinline__ void octet_job(const KC& kc, const tg_batch& b,
             const uint4 wc = win ? win_consts<NR>(lane4, rkT, cc, c0) : make_uint4(0, 0, 0, 0);
 #pragma unroll
             for (int h = 0; h < 2; ++h) {
+                if (h == 1 && __all(!valid || nvl <= 8u * beta + 4u)) break;
                 uint4 ks[4];
                 t_half<NR>(lane4, rkT, cc, c0, win, wc, k0w, h, ks);
                 consume(ks, blk0, 4 * h, std::integral_constant<int, 4>());
                 __builtin_amdgcn_sched_barrier(0);
             }
+        } else if (!OPEN && one) {
+            // slot 0 only: E_K(nonce || c0) byte-wise (the tag mask's path);
+            // consume() XORs the last round key again
+            const uint4 nvr = valid ? load_partial(b.nonce + 12 * i, 12) : make_uint4(0, 0, 0, 0);
+            uint4 ks[1] = {xor4(aes_block_sb<NR>(rk, make_uint4(nvr.x, nvr.y, nvr.z, bswap32(c0)), sbox), rkl)};
+            consume(ks, blk0, 0, std::integral_constant<int, 1>());
         } else {
             uint32_t s[4][8];
 #pragma unroll

@@ -83,6 +83,24 @@ __device__ __forceinline__ void gstore16(uint8_t* p, uint4 v) {
 #endif
 }
 
+// The same at any byte address: one global_load/store_dwordx4 with the byte
+// offset (amdhsa runs gfx9 in unaligned-access mode), instead of 16 byte
+// accesses -- records behind a 5-byte TLS header are never 16-byte aligned.
+typedef u32x4 u32x4_u1 __attribute__((aligned(1)));
+__device__ __forceinline__ uint4 gload16u(const uint8_t* p) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    const u32x4 v = *(const __attribute__((address_space(1))) u32x4_u1*)p;
+    return make_uint4(v.x, v.y, v.z, v.w);
+#else
+    return uint4();
+#endif
+}
+__device__ __forceinline__ void gstore16u(uint8_t* p, uint4 v) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    *(__attribute__((address_space(1))) u32x4_u1*)p = u32x4{v.x, v.y, v.z, v.w};
+#endif
+}
+
 __device__ __forceinline__ uint4 xor4(uint4 a, uint4 b) {
     return make_uint4(a.x ^ b.x, a.y ^ b.y, a.z ^ b.z, a.w ^ b.w);
 }
@@ -162,15 +180,14 @@ __device__ __forceinline__ void store_partial(uint8_t* p, uint4 v, uint32_t n) {
 
 // Full 16-byte block; the vector form when the record is 16-byte aligned.
 __device__ __forceinline__ uint4 load16(const uint8_t* p, bool aligned) {
-    if (aligned) return gload16(p);
-    return load_partial(p, 16);
+    return aligned ? gload16(p) : gload16u(p);
 }
 
 __device__ __forceinline__ void store16(uint8_t* p, uint4 v, bool aligned) {
     if (aligned) {
         gstore16(p, v);
     } else {
-        store_partial(p, v, 16);
+        gstore16u(p, v);
     }
 }
 

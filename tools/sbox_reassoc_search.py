@@ -5,7 +5,7 @@ gate, kept when the minimum cover does not grow).  Each cover is a 0/1
 program of ~20 s; round 2 ran seeds 11-14 x 150 steps (about an hour on four
 cores), all ending at 72 gates (from 74), and took one of them as REASSOC.
 
-    python3 tools/sbox_reassoc_search.py SEED STEPS > gates.json
+    python3 tools/sbox_reassoc_search.py SEED STEPS [UPHILL] > gates.json
 """
 import json
 import os
@@ -48,19 +48,25 @@ def main():
     seed, steps = int(sys.argv[1]), int(sys.argv[2])
     rng = random.Random(seed)
     cur = gb.parse(gb.CIRCUIT)
+    if os.environ.get("SBOX_FROM_REASSOC"):   # continue from the shipped re-association
+        cur.update(gb.parse(gb.REASSOC))
     best = cover_size(cur)
     print("start %d" % best, file=sys.stderr, flush=True)
+    # annealing: a cover one gate larger is accepted with probability ``uphill``
+    uphill = float(sys.argv[3]) if len(sys.argv) > 3 else 0.0
+    cur_c, top = best, cur
     for it in range(steps):
         g = cur
         for _ in range(rng.randint(1, 3)):
             g = apply(g, rng.choice(moves(g)), rng.randint(0, 1))
         c = cover_size(g)
-        if c <= best:
+        if c <= cur_c or (c == cur_c + 1 and rng.random() < uphill):
+            cur, cur_c = g, c
             if c < best:
                 print("step %d -> %d" % (it, c), file=sys.stderr, flush=True)
-            best, cur = c, g
-    gb.check(cur, gb.topo(cur))
-    json.dump({"gates": best, "circuit": {k: list(v) for k, v in cur.items()}}, sys.stdout)
+                best, top = c, g
+    gb.check(top, gb.topo(top))
+    json.dump({"gates": best, "circuit": {k: list(v) for k, v in top.items()}}, sys.stdout)
 
 
 if __name__ == "__main__":
