@@ -130,13 +130,16 @@ __device__ __forceinline__ void tiled_blocks(WaveTile& t, uint32_t lane, uint32_
     const uint32_t grp = lane >> 5, cq = lane & 7u, rq = lane >> 3;
     // the coalesced ops of group g's pair starting at block p0 (even)
     auto load_pair = [&](uint32_t g, uint32_t p0, uint4 (&R)[4]) {
-        const uint32_t blk = p0 + (cq >> 2);
+        // unconditional: a chunk past the tile's blocks re-reads block 0 of
+        // its record (rows past the batch hold the last record's pointers),
+        // so no branch leaves a load into R pending on some paths only
+        const uint32_t off = p0 + (cq >> 2) < jmin ? 64 * p0 + 16 * cq : 16 * (cq & 3u);
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
             const uint32_t r = 32 * g + 8 * q + rq;
             const uint4 pr = t.ptr[r];
             const uint8_t* src = reinterpret_cast<const uint8_t*>(((uint64_t)pr.y << 32) | pr.x);
-            if (r < nvalid && blk < jmin) R[q] = gload16(src + 64 * p0 + 16 * cq);
+            R[q] = gload16(src + off);
         }
     };
     auto put_pair = [&](uint32_t g, const uint4 (&R)[4]) {
@@ -157,14 +160,43 @@ __device__ __forceinline__ void tiled_blocks(WaveTile& t, uint32_t lane, uint32_
             if (r < nvalid && blk < jmin) gstore16(dst + 64 * p0 + 16 * cq, v);
         }
     };
+    // The pair finished in iteration i is stored at the top of iteration
+    // i + 1: its rows are read before put_pair overwrites them and the global
+    // stores go out right after it, so the next iteration's vmcnt(0) (loads
+    // and stores share the counter) waits for stores issued a whole
+    // iteration earlier instead of one ChaCha block earlier.
+    auto flush_pair = [&](uint32_t g, uint32_t p0, const uint4 (&S)[4]) {
+        const uint32_t blk = p0 + (cq >> 2);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const uint32_t r = 32 * g + 8 * q + rq;
+            const uint4 pr = t.ptr[r];
+            uint8_t* dst = reinterpret_cast<uint8_t*>(((uint64_t)pr.w << 32) | pr.z);
+            if (r < nvalid && blk < jmin) gstore16(dst + 64 * p0 + 16 * cq, S[q]);
+        }
+    };
+    auto read_pair = [&](uint32_t g, uint4 (&S)[4]) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const uint32_t r = 32 * g + 8 * q + rq;
+            S[q] = t.row[r][swz(r, cq)];
+        }
+    };
     uint4 R[4];
     load_pair(0, 0, R);
     for (uint32_t i = 0; i <= jmin; ++i) {
         // group A's pair (i, i + 1) at even i, group B's (i - 1, i) at odd i
         const uint32_t g = i & 1u, p0 = i - g;
-        if (p0 < jmin) put_pair(g, R);
+        // the pair finished in iteration i - 1: group A's (i - 2, i - 1) at
+        // even i >= 2, group B's (i - 3, i - 2) at odd i >= 3
+        const bool fl = (i >= 2 && !(i & 1u)) || (i >= 3 && (i & 1u));
+        const uint32_t fg = i & 1u, fp = (i & 1u) ? i - 3 : i - 2;
+        uint4 S[4];
+        if (fl) read_pair(fg, S);
+        put_pair(g, R);   // past the last pair: the group's rows are free (read above)
+        if (fl) flush_pair(fg, fp, S);
         __builtin_amdgcn_wave_barrier();
-        if (i + 1 - ((i + 1) & 1u) < jmin) load_pair((i + 1) & 1u, i + 1 - ((i + 1) & 1u), R);
+        load_pair((i + 1) & 1u, i + 1 - ((i + 1) & 1u), R);
         const uint32_t b = i - grp;                 // this lane's block
         const bool act = i >= grp && b < jmin;
         uint4 m[4];
@@ -180,19 +212,17 @@ __device__ __forceinline__ void tiled_blocks(WaveTile& t, uint32_t lane, uint32_
             }
         }
         __builtin_amdgcn_wave_barrier();
-        // the pair finished now: group A's (i - 1, i) at odd i, group B's
-        // (i - 2, i - 1) at even i >= 2
-        if (i & 1u) {
-            store_pair(0, i - 1);
-        } else if (i >= 2) {
-            store_pair(1, i - 2);
-        }
-        __builtin_amdgcn_wave_barrier();
         if (act) {
             chacha_block(k, b + 2, nv.x, nv.y, nv.z, ks);
 #pragma unroll
             for (int c = 0; c < 4; ++c) poly_block(p, m[c]);
         }
+    }
+    // the pair finished in the last iteration (i = jmin)
+    if (jmin & 1u) {
+        store_pair(0, jmin - 1);
+    } else if (jmin >= 2) {
+        store_pair(1, jmin - 2);
     }
     // group B's last pair when jmin is odd (its block jmin - 1 ran at iteration jmin)
     if (jmin & 1u) store_pair(1, jmin - 1);
