@@ -210,14 +210,15 @@ __device__ __forceinline__ void octet_job(const KC& kc, const tg_batch& b,
                                          rk[4 * NR + 2] ^ 0x63636363u, rk[4 * NR + 3] ^ 0x63636363u);
     // XOR + store of N consecutive slots j0 .. j0 + N - 1 (the keystream dies
     // block by block), then the GHASH chain over their inputs
-    auto consume = [&](const uint4* ks, uint32_t blk0, int j0, auto NN) {
+    // pre: the slots' payload already loaded (fast path only), else nullptr
+    auto consume = [&](const uint4* ks, uint32_t blk0, int j0, auto NN, const uint4* pre) {
         constexpr int N = decltype(NN)::value;
         if (blk0 < (nfast << 6)) {   // every valid lane of the wave has these blocks full
             if (valid) {
                 uint4 d[N];
 #pragma unroll
                 for (int q = 0; q < N; ++q)
-                    d[q] = gload16u(in + 16u * (blk0 + 8u * (j0 + q)));
+                    d[q] = pre ? pre[q] : gload16u(in + 16u * (blk0 + 8u * (j0 + q)));
 #pragma unroll
                 for (int q = 0; q < N; ++q) {
                     const uint4 k = ks[q];
@@ -270,8 +271,16 @@ __device__ __forceinline__ void octet_job(const KC& kc, const tg_batch& b,
             for (int h = 0; h < 2; ++h) {
                 if (h == 1 && __all(!valid || nvl <= 8u * beta + 4u)) break;
                 uint4 ks[4];
+                // the half's payload is loaded before its keystream is computed
+                // (1.3 / 0.6 % for seal / open, profiles/r02/v70_tprefetch/)
+                uint4 dp[4];
+                const bool fast = blk0 < (nfast << 6);
+                if (fast && valid) {
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) dp[q] = gload16u(in + 16u * (blk0 + 8u * (4 * h + q)));
+                }
                 t_half<NR>(lane4, rkT, cc, c0, win, wc, k0w, h, ks);
-                consume(ks, blk0, 4 * h, std::integral_constant<int, 4>());
+                consume(ks, blk0, 4 * h, std::integral_constant<int, 4>(), fast ? dp : nullptr);
                 __builtin_amdgcn_sched_barrier(0);
             }
         } else if (!OPEN && one) {
@@ -279,7 +288,7 @@ __device__ __forceinline__ void octet_job(const KC& kc, const tg_batch& b,
             // consume() XORs the last round key again
             const uint4 nvr = valid ? load_partial(b.nonce + 12 * i, 12) : make_uint4(0, 0, 0, 0);
             uint4 ks[1] = {xor4(aes_block_sb<NR>(rk, make_uint4(nvr.x, nvr.y, nvr.z, bswap32(c0)), sbox), rkl)};
-            consume(ks, blk0, 0, std::integral_constant<int, 1>());
+            consume(ks, blk0, 0, std::integral_constant<int, 1>(), nullptr);
         } else {
             uint32_t s[4][8];
 #pragma unroll
@@ -301,7 +310,9 @@ __device__ __forceinline__ void octet_job(const KC& kc, const tg_batch& b,
             uint4 ks[8];
 #pragma unroll
             for (int j = 0; j < 8; ++j) ks[j] = make_uint4(w[0][j], w[1][j], w[2][j], w[3][j]);
-            consume(ks, blk0, 0, std::integral_constant<int, 8>());
+            // (loading the payload before encrypt() too would keep 32 more
+            // VGPRs live across it: 270 spilled registers in the seal kernel)
+            consume(ks, blk0, 0, std::integral_constant<int, 8>(), nullptr);
         }
     }
     if (!__any(valid)) return;
