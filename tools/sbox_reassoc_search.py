@@ -3,7 +3,9 @@ the exact 3-input gate cover of tools/gen_bs_sbox.py (random hill climb: 1-3
 moves (a ^ b) ^ c -> (a ^ c) ^ b or (b ^ c) ^ a, where a ^ b feeds only this
 gate, kept when the minimum cover does not grow).  Each cover is a 0/1
 program of ~20 s; round 2 ran seeds 11-14 x 150 steps (about an hour on four
-cores), all ending at 72 gates (from 74), and took one of them as REASSOC.
+cores), all ending at 72 gates (from 74), and took one of them as REASSOC;
+annealing from that circuit (SBOX_FROM_REASSOC=1, seeds 21-24, uphill 0.25,
+~75 minutes each) found nothing below 72.
 
     python3 tools/sbox_reassoc_search.py SEED STEPS [UPHILL] > gates.json
 """
