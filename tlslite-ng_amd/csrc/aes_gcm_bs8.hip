@@ -130,7 +130,10 @@ struct SingleKeyCtx {   // one key for the batch: 8-bit H^8 tables in LDS (gmul_
     __device__ __forceinline__ uint4 hpow(int e) const { return key->hpow[e - 1]; }
     __device__ __forceinline__ uint4 gmul(uint4 y) const { return gmul_rot(y, threadIdx.x & 15u, jt); }
 };
-struct SingleKeyRowCtx {   // SingleKeyCtx with the lane's offset row held in registers
+// SingleKeyCtx with the lane's offset row held in registers (the hybrid
+// kernel's waves of both roles: one ds_read_b128 fewer per block; T-table
+// waves ~0.3 %, profiles/r02/v52_ghash_row/; bitsliced ~0.5 %, v76_bs_row/)
+struct SingleKeyRowCtx {
     const GcmKeyDev* key;
     uint4 jw;
     __device__ __forceinline__ const uint32_t* rk() const { return key->rk; }
@@ -439,16 +442,16 @@ __global__ __launch_bounds__(kHyThreads) void gcm_hy_kernel(const GcmKeyDev* __r
             asm volatile("" ::: "memory");
             const tg_batch b = *bp;
             if (KEYS == 0)
-                octet_job<NR, OPEN, false>(SingleKeyCtx{key, kHyJt}, b, order, 8ull * job, recw,
+                octet_job<NR, OPEN, false>(SingleKeyRowCtx{key, jw}, b, order, 8ull * job, recw,
                                            none, kHySbox, bs8::KeyPlanesLds{kHyKeys});
             else if (KEYS == 2)
-                octet_job<NR, OPEN, false>(SingleKeyCtx{key, kHyJt}, b, order, 8ull * job, recw,
+                octet_job<NR, OPEN, false>(SingleKeyRowCtx{key, jw}, b, order, 8ull * job, recw,
                                            none, kHySbox, bs8::KeyPlanesVmem{krows});
             else if (KEYS == 4)
-                octet_job<NR, OPEN, false>(SingleKeyCtx{key, kHyJt}, b, order, 8ull * job, recw,
+                octet_job<NR, OPEN, false>(SingleKeyRowCtx{key, jw}, b, order, 8ull * job, recw,
                                            none, kHySbox, bs8::KeyPlanesVmemFolded{{krows}});
             else
-                octet_job<NR, OPEN, false>(SingleKeyCtx{key, kHyJt}, b, order, 8ull * job, recw,
+                octet_job<NR, OPEN, false>(SingleKeyRowCtx{key, jw}, b, order, 8ull * job, recw,
                                            none, kHySbox, bs8::KeyPlanes{key->bs8mask});
         }
     }
