@@ -84,10 +84,13 @@ def _cpu_worker(L, seed, seconds, start, q):
 
 
 def cpu_baseline(L, cores, seconds, gpu_samples):
-    """The reference's pure-Python path (oracle/pyaead.py restates it; it runs
-    at 0.6-1.0x the reference's own per-core speed) on ``cores``
-    host processes started together, each sealing and opening L-byte records
-    with both AEADs for ``seconds``.  The same leg re-seals ``gpu_samples``
+    """The reference's pure-Python path, restated in oracle/pyaead.py, on
+    ``cores`` host processes started together, each sealing and opening
+    L-byte records with both AEADs for ``seconds``.  pyaead is not slower
+    than the reference: a 16 KiB seal takes 44.4 ms against the reference's
+    63.5 ms for AES-128-GCM (1.43x faster) and 39.9 against 37.3 ms for
+    ChaCha20-Poly1305 (0.93x; tests/golden/make_golden.py --timing), so this
+    baseline overstates the reference's own CPU rate, if anything.  The same leg re-seals ``gpu_samples``
     (records the GPU sealed in this run: key, nonce, plaintext, GPU output)
     and reports whether the GPU bytes match."""
     ctx = mp.get_context("spawn")
@@ -125,6 +128,35 @@ def read_bytes(n, L, op):
     return n * (L + AAD_LEN + NONCE_LEN + (TAG_LEN if op == "open" else 0))
 
 
+def free_port():
+    """A TCP port free on 127.0.0.1 right now (the rendezvous of the ranks)."""
+    import socket
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        return so.getsockname()[1]
+
+
+def rank_launch_cmd(argv, gpus, port):
+    """The command that runs this bench as ``gpus`` ranks, one process per
+    GPU: torch.distributed.run on one node, rendezvous on 127.0.0.1, the
+    same bench arguments.  (The driver's own N > 1 runs start the ranks
+    themselves; then WORLD_SIZE is set and no launch happens.)"""
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node",
+            str(gpus), "--master-addr", "127.0.0.1", "--master-port", str(port),
+            os.path.abspath(__file__)] + list(argv)
+
+
+def check_world(gpus, env=None):
+    """Inside a rank: the launcher's world size must be what --gpus asked
+    for.  Returns an error message or None."""
+    env = os.environ if env is None else env
+    world = int(env.get("WORLD_SIZE", "1"))
+    if world != gpus:
+        return "--gpus %d but WORLD_SIZE=%d: launch one rank per GPU (bench.py --gpus N starts them)" % (
+            gpus, world)
+    return None
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -155,6 +187,21 @@ def main():
     ap.add_argument("--ingest-mib", type=int, default=2048,
                     help="application data per direction for --config ingest")
     args = ap.parse_args()
+    if args.gpus < 1:
+        ap.error("--gpus must be >= 1")
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        # N ranks, one process per GPU, started here before anything in this
+        # process touches the GPU; this process only waits and passes on the
+        # ranks' exit status (rank 0 prints the JSON line)
+        if args.config in ("c4", "ingest"):
+            ap.error("--config %s runs on one GPU (BASELINE configs[3] / the host pipeline)" % args.config)
+        import subprocess
+        sys.stdout.flush()
+        sys.exit(subprocess.call(rank_launch_cmd(sys.argv[1:], args.gpus, free_port())))
+    err = check_world(args.gpus)
+    if err:
+        print(err, file=sys.stderr)
+        sys.exit(2)
     if args.config == "ingest":
         return run_ingest(args)
     if args.config == "c4":
@@ -344,32 +391,128 @@ def c5_algorithmic_bytes(n, L_app, op):
     return n * (L_app + wire) if op == "seal" else n * (wire + L_app + 1 + 6)
 
 
+C5_APP = 16384
+
+
+def c5_layout(L=C5_APP):
+    """Config 5's buffers: fragment i at i * DS (DS = L + 1 rounded up to a
+    128-byte line: the inner content type is appended in place), wire record
+    i at i * WS + 123, so its ciphertext after the 5-byte header starts on a
+    128-byte line.  Returns (DS, WS, header offset)."""
+    DS = (L + 1 + 127) // 128 * 128
+    WS = (5 + L + 1 + TAG_LEN + 123 + 127) // 128 * 128
+    return DS, WS, 123
+
+
+def c5_pick(n, count=128, seed=0xc5):
+    """Records checked against the framing oracle: the first, the last and
+    random others (count in all, fewer when n is smaller)."""
+    import numpy as np
+    rng = np.random.default_rng(seed)
+    idx = set([0, n - 1])
+    while len(idx) < min(count, n):
+        idx.add(int(rng.integers(0, n)))
+    return sorted(idx)
+
+
+def c5_samples(data, wire, wire_len, idx, L=C5_APP):
+    """Host copies of the picked records: (i, fragment, wire record)."""
+    DS, WS, H = c5_layout(L)
+    wl = wire_len.cpu().numpy()
+    out = []
+    for i in idx:
+        frag = data[i * DS:i * DS + L].cpu().numpy().tobytes()
+        w = wire[i * WS + H:i * WS + H + int(wl[i])].cpu().numpy().tobytes()
+        out.append((i, frag, w))
+    return out
+
+
+def c5_check(samples, key, iv, seq0):
+    """CPU leg, checker part: every sampled wire record equals
+    oracle/records.seal_record (recordlayer.py:606-617, :536-565 restated,
+    pinned to the reference RecordLayer's wire bytes) for its seq, and opens
+    back there to (ok, 0x17, fragment).  Returns the number of mismatches."""
+    sys.path.insert(0, ROOT)
+    from oracle import records as R
+    bad = 0
+    for i, frag, w in samples:
+        want = R.seal_record("tls13", "aes128gcm", key, iv, seq0 + i, 0x17, frag)
+        got_open = R.open_record("tls13", "aes128gcm", key, iv, seq0 + i, w)
+        bad += int(w != want or got_open != (R.OK, 0x17, frag))
+    return bad
+
+
+def _cpu_worker_c5(L, seed, seconds, start, q):
+    """sendRecord + _encryptThenSeal for TLS 1.3 AES-128-GCM (recordlayer.py:
+    606-617, :536-565) with the pure-Python AEAD restatement."""
+    sys.path.insert(0, ROOT)
+    import numpy as np
+    from oracle import pyaead
+    from vectors import tls13_nonce
+    rng = np.random.default_rng(seed)
+    c = pyaead.AESGCM(rng.bytes(16))
+    iv = rng.bytes(12)
+    data = rng.bytes(L)
+    start.wait()
+    t0 = time.perf_counter()
+    done, i = 0, 0
+    while time.perf_counter() - t0 < seconds:
+        inner = data + b"\x17"
+        n = len(inner) + TAG_LEN
+        hdr = bytes([0x17, 3, 3, n >> 8, n & 0xff])
+        wire = hdr + bytes(c.seal(tls13_nonce(iv, i), inner, hdr))
+        assert len(wire) == 5 + n
+        done += L
+        i += 1
+    q.put((done, time.perf_counter() - t0))
+
+
+def cpu_baseline_c5(L, cores, seconds):
+    ctx = mp.get_context("spawn")
+    start, q = ctx.Barrier(cores + 1), ctx.Queue()
+    procs = [ctx.Process(target=_cpu_worker_c5, args=(L, 2000 + c, seconds, start, q))
+             for c in range(cores)]
+    for p in procs:
+        p.start()
+    start.wait()
+    res = [q.get() for _ in procs]
+    for p in procs:
+        p.join()
+    total = sum(r[0] for r in res)
+    wall = max(r[1] for r in res)
+    cap, ncpu = host_cores()
+    return {"value": total / wall / 2 ** 30, "unit": "GiB/s", "cores": cores, "kind": "port",
+            "host_cpus": ncpu, "usable_cpus": cap,
+            "sample": "%d processes x %.0f s each, TLS 1.3 AES-128-GCM record seal (inner type, "
+                      "header, AEAD) of %d-byte fragments, oracle/pyaead.py (pure-Python restatement "
+                      "of the reference path)" % (cores, seconds, L)}
+
+
 def run_config5(args):
     """BASELINE configs[4]: TLS 1.3 AES-128-GCM record seal, 2^20 records per
     GPU of L = 16384 application bytes through the device framing path
     (tg_seal_records: inner plaintext = data || 0x17, header 17 03 03 40 11,
     ct || tag behind it; recordlayer.py:606-617, :536-565); rank g seals seq
     [g 2^20, (g + 1) 2^20) of one connection (tlsgpu.distributed).  RCCL
-    carries only the counters.  Checked (untimed) by opening the wire records
-    back with tg_open_records (status, content type, plaintext)."""
-    import numpy as np
+    carries only the counters.  Checked (untimed) by opening every wire record
+    back with tg_open_records (status, content type, plaintext), and on rank 0
+    by the CPU leg: 128 sampled wire records (the first and the last among
+    them) compared byte for byte with the framing oracle."""
     import torch
     import torch.distributed as dist
     import tlsgpu
     from tlsgpu import distributed as tgd
     world, rank, _, _ = tgd.init_process(torch, dist)
-    n, L = args.records, 16384
+    n, L = args.records, C5_APP
     first, _ = tgd.weak_shard(n, world, rank)
-    DS = (L + 1 + 127) // 128 * 128                 # data slot: fragment + inner type
-    WS = (5 + L + 1 + TAG_LEN + 123 + 127) // 128 * 128
+    DS, WS, H = c5_layout(L)
     g = torch.Generator(device="cuda").manual_seed(0x7715 + rank)
     data = torch.randint(0, 256, (n * DS,), dtype=torch.uint8, device="cuda", generator=g)
     orig = data.view(n, DS)[:, :L].clone()
     data_off = torch.arange(n, dtype=torch.int64, device="cuda") * DS
     data_len = torch.full((n,), L, dtype=torch.int32, device="cuda")
     ctype = torch.full((n,), 0x17, dtype=torch.uint8, device="cuda")
-    # the ciphertext after the 5-byte header starts on a 128-byte line
-    wire_off = torch.arange(n, dtype=torch.int64, device="cuda") * WS + 123
+    wire_off = torch.arange(n, dtype=torch.int64, device="cuda") * WS + H
     wire = torch.empty(n * WS, dtype=torch.uint8, device="cuda")
     wire_len = torch.zeros(n, dtype=torch.int32, device="cuda")
     hrng = torch.Generator().manual_seed(0x7716)
@@ -394,6 +537,7 @@ def run_config5(args):
     elapsed = tgd.timed(torch, dist, world, lambda s: step(True), args.steps)
     # untimed check: every wire record opens back to its fragment and type
     wl = int(wire_len[0].item())
+    samples = c5_samples(data, wire, wire_len, c5_pick(n), L) if rank == 0 else []
     back = torch.zeros(n * DS, dtype=torch.uint8, device="cuda")
     o_len = torch.zeros(n, dtype=torch.int32, device="cuda")
     o_ct = torch.zeros(n, dtype=torch.uint8, device="cuda")
@@ -404,14 +548,16 @@ def run_config5(args):
     ok = (bool((wire_len == 5 + L + 1 + TAG_LEN).all()) and int((st == 0).sum()) == n and
           bool((o_ct == 0x17).all()) and bool((o_len == L).all()) and
           bool(torch.equal(back.view(n, DS)[:, :L], orig)))
-    hdr = wire[123:128].cpu().numpy().tobytes()
+    hdr = wire[H:H + 5].cpu().numpy().tobytes()
     ok = ok and hdr == bytes([0x17, 0x03, 0x03, (L + 17) >> 8, (L + 17) & 0xff])
     sums, elapsed = tgd.reduce_counters(torch, dist, [n * args.steps, n * L * args.steps, 0],
                                         elapsed, device="cuda")
     ms = sum(a.elapsed_time(b) for a, b in evs) / len(evs)
     ach = c5_algorithmic_bytes(n, L, "seal") / (ms / 1e3) / 1e9
     if rank == 0:
-        print(json.dumps({
+        bad = c5_check(samples, key, iv, first)
+        ok = ok and bad == 0
+        line = {
             "metric": "GiB/s device-resident TLS 1.3 AES-128-GCM record seal (BASELINE configs[4])",
             "value": round(sums[1] / elapsed / 2 ** 30, 2), "unit": "GiB/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup,
@@ -419,14 +565,20 @@ def run_config5(args):
             "scaling": "weak", "dtype": "u8", "data": "synthetic",
             "config": {"workload": "configs[4]: tg_seal_records (header + inner type + AEAD)",
                        "records_per_gpu": n, "app_bytes": L, "wire_record": wl,
-                       "records_total": int(sums[0] / args.steps)},
+                       "records_total": int(sums[0] / args.steps),
+                       "layout": "fragment stride %d, wire stride %d, header at +%d" % (DS, WS, H)},
             "roofline": {"bound": "hbm", "kernel": "seal_records (framing + AEAD launches)",
                          "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(ach / HBM_PEAK_GBS, 4),
                          "frac_read": round(n * L / (ms / 1e3) / 1e9 / HBM_PEAK_GBS, 4),
                          "bytes_per_record": c5_algorithmic_bytes(1, L, "seal"), "traffic": None,
                          "ms": round(ms, 3)},
-            "verified": bool(ok)}), flush=True)
+            "oracle_checked_records": len(samples), "oracle_mismatches": bad,
+            "verified": bool(ok)}
+        if not args.no_cpu_baseline and world == 1:
+            cores = args.cpu_cores or host_cores()[0]
+            line["cpu_baseline"] = cpu_baseline_c5(L, cores, args.cpu_seconds)
+        print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
     if not ok:

@@ -13,10 +13,12 @@
  * Conventions: plain pointers and sizes, no exceptions across the ABI, every
  * function returns an int status (TG_OK = 0, negative = error; tg_open
  * returns 1 = authentic / 0 = rejected).  A key handle is bound to the device
- * current when it was created and is not thread-safe (one handle per
- * connection direction, as ConnectionState.encContext is in the reference,
- * recordlayer.py:239-249).  Batch entry points take DEVICE pointers and are
- * ordered on the given HIP stream (NULL = the null stream).
+ * current when it was created.  tg_seal / tg_open may be called on one handle
+ * from several threads at once (each call takes its own staging slot: copies
+ * of an AEAD object share the handle, recordlayer.py:262, :913);
+ * tg_key_destroy must not race with calls on the same handle.  Batch entry
+ * points take DEVICE pointers and are ordered on the given HIP stream (NULL =
+ * the null stream).
  */
 #ifndef TLSGPU_H
 #define TLSGPU_H
@@ -56,6 +58,26 @@ const char* tg_last_error(void);           /* thread-local message of the last e
 int tg_device_count(int* count);
 int tg_init(int device);                   /* hipSetDevice for the calling thread */
 
+/* Kernel-selection options (process-wide; tests and measurement -- the
+ * engine's own choice is value 0 everywhere).  Each starts from its TLSGPU_*
+ * environment variable, read once at first use:
+ *   gcm_variant        0 auto, 6 wave per record, 14 bitsliced octet,
+ *                      15 hybrid octet, 16 T-table lane per record
+ *   gcm_table_variant  0 auto (length split), 1 lane, 5 wave per record,
+ *                      14 key-grouped octet
+ *   kt_split           key-table length split in bytes (0 = 2048)
+ *   chacha_variant     0 auto, 3 wave per record, 4 lane per record
+ *   ccm_variant        0 auto, 1 lane full rounds, 2 wave, 3 lane
+ *   waves_per_record   0 auto, 1 / 4 / 16
+ *   no_plan            1 = no length-sorted launch order
+ *   stage_copy         1 = per-record calls copy through device memory
+ *   hy_t, hy_noprio    hybrid AES-GCM kernel: T-table waves (0 = 8 of 16),
+ *                      1 = T-table waves at normal priority
+ * An unknown name is TG_EINVAL; a variant a launcher does not know makes
+ * its launches fail with TG_EINVAL. */
+int tg_set_option(const char* name, int value);
+int tg_get_option(const char* name, int* value);
+
 /* Keys -- replaces python_aesgcm.new (python_aesgcm.py:10-11) and
  * python_chacha20_poly1305.new (python_chacha20_poly1305.py:9-11): expands the
  * AES round keys and the GHASH tables for H = E_K(0) (aesgcm.py:27-57) on the
@@ -93,7 +115,9 @@ int tg_open(tg_key* k, const uint8_t* nonce, size_t noncelen,
  *   nonce    nonce + 12 * i (12 bytes)
  *   aad      aad + (aad_off ? aad_off[i] : i * aad_stride),
  *            aad_len ? aad_len[i] : fixed_aad_len bytes
- *   key      key table entry key_idx ? key_idx[i] : 0
+ *   key      key table entry key_idx ? key_idx[i] : 0; key_idx[i] must be
+ *            below the table's nkeys -- a record with an index out of range
+ *            is skipped (never read past the table; open: status[i] = 0)
  *   status   open only: status[i] = 1 authentic / 0 rejected (pt zeroed)
  * len == NULL means every record is fixed_len bytes.  Offsets with 16-byte
  * alignment take the vector path; any alignment is accepted.

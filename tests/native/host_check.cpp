@@ -115,8 +115,6 @@ static int check_keys() {
                 CHECK(memcmp(w, tab[e], 16) == 0, "H^%d table entry %d", which ? 64 : 8, e);
             }
         }
-        for (int e = 0; e < 128 * (nr + 1); ++e)
-            CHECK(img->bsmask[e] == bs_mask_word(img->rk, e), "bsmask %d", e);
         for (int e = 0; e < 32 * (nr + 1); ++e)
             CHECK(img->bs8mask[e] == bs8_mask_word(img->rk, e), "bs8mask %d", e);
         delete img;

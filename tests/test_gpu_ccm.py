@@ -102,32 +102,25 @@ def test_batch_ragged_vs_oracle(torch, tg, oracle_mod, klen, tl, align, variant)
     lens = LEN_MIX * 4 + list(rng.integers(0, 16401, 150)) + [65520, 65536, 70001]
     hb = HostBatch(lens, payload_seed=align + tl, align=align, aad_mode="random", tag=tl)
     key = rng.bytes(klen)
-    old = os.environ.get("TLSGPU_CCM_VARIANT")
-    os.environ["TLSGPU_CCM_VARIANT"] = variant
-    try:
+    with tg.options(ccm_variant=int(variant)):
         run_seal_open(torch, tg, oracle_mod, hb, "aesccm" if tl == 16 else "aesccm8",
                       np.frombuffer(key, np.uint8), _obj(tg, key, tl), tamper=(3, 17, 100))
-    finally:
-        if old is None:
-            del os.environ["TLSGPU_CCM_VARIANT"]
-        else:
-            os.environ["TLSGPU_CCM_VARIANT"] = old
 
 
 @pytest.mark.parametrize("klen,tl", [(16, 16), (32, 8)])
 @pytest.mark.parametrize("align", [16, 1])
 @pytest.mark.parametrize("variant", ["2", "3"])   # wave per record / lane per record
-def test_key_table_vs_oracle(torch, tg, oracle_mod, klen, tl, align, variant, monkeypatch):
+def test_key_table_vs_oracle(torch, tg, oracle_mod, klen, tl, align, variant):
     from batchpack import HostBatch, run_seal_open
-    monkeypatch.setenv("TLSGPU_CCM_VARIANT", variant)
     rng = np.random.default_rng(3 + klen + tl + align)
     lens = list(rng.integers(0, 4097, 700)) + [0, 1, 15, 16, 17, 16384, 16400]
     hb = HostBatch(lens, payload_seed=4, align=align, aad_mode="tls12", key_count=29, tag=tl)
     keys = [rng.bytes(klen) for _ in range(29)]
     table = tg.KeyTable("aesccm" if tl == 16 else "aesccm_8", keys)
     karr = np.frombuffer(b"".join(keys), np.uint8).reshape(29, klen)
-    run_seal_open(torch, tg, oracle_mod, hb, "aesccm" if tl == 16 else "aesccm8", karr, table,
-                  tamper=(1, 500))
+    with tg.options(ccm_variant=int(variant)):
+        run_seal_open(torch, tg, oracle_mod, hb, "aesccm" if tl == 16 else "aesccm8", karr, table,
+                      tamper=(1, 500))
 
 
 @pytest.mark.parametrize("bi", range(4))

@@ -10,13 +10,19 @@ import pytest
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.parametrize("variant", ["0", "14"])   # lane kernel / key-grouped octet kernel
-def test_config4_full_shape_sampled(oracle_mod, variant, monkeypatch):
+# auto (length split: octet kernel for the long records, lane kernel for the
+# rest) / lane kernel for all / key-grouped octet kernel for all
+@pytest.mark.parametrize("variant", [0, 1, 14])
+def test_config4_full_shape_sampled(oracle_mod, variant):
     import torch
     import tlsgpu
-    monkeypatch.setenv("TLSGPU_GCM_TABLE_VARIANT", variant)
     if not torch.cuda.is_available():
         pytest.fail("GPU tests need a visible MI355X")
+    with tlsgpu.options(gcm_table_variant=variant):
+        _run_config4(torch, tlsgpu, oracle_mod)
+
+
+def _run_config4(torch, tlsgpu, oracle_mod):
     n, nkeys = 1 << 20, 65536
     rk = np.random.default_rng(0x7716)
     keys = rk.integers(0, 256, (nkeys, 32), dtype=np.uint8)

@@ -239,3 +239,36 @@ def test_read_application_data_errors(torch, tg, batch):
     r.feed(bytes([23, 3, 3, 0x41, 0x01]))
     with pytest.raises(TLSRecordOverflow):
         r.read_application_data()
+
+
+@pytest.mark.parametrize("out_kind", ["pageable", "pinned"])
+@pytest.mark.parametrize("batch", [2, 5, 1024])
+def test_read_application_data_out_too_small_retry(torch, tg, out_kind, batch):
+    """A caller buffer too small for the data is a ValueError that changes
+    nothing: a retry with a large enough buffer returns exactly the bytes a
+    first call with it would have (sequence numbers and the unread wire bytes
+    are restored); the stream goes on after it, including a bad
+    record's error at its place."""
+    from tlsgpu.ingest import TLSBadRecordMAC
+    key, iv = detbytes("small-out", 16), detbytes("small-out-iv", 12)
+    recs, app = _mixed_stream(key, iv, 30, 3 + batch, bad=27)
+    want = b"".join(app[:27])
+    r = tg.RecordReader(_key(tg, "aesgcm", key), tg.TLS13, iv, batch_records=batch)
+    r.feed(b"".join(recs[:20]))
+    first = len(b"".join(app[:20]))
+    mk = (lambda n: torch.empty(n, dtype=torch.uint8).pin_memory().numpy()) if out_kind == "pinned" \
+        else (lambda n: np.zeros(n, np.uint8))
+    if first:
+        small = mk(max(1, first // 3))
+        with pytest.raises(ValueError):
+            r.read_application_data(out=memoryview(small))
+        with pytest.raises(ValueError):   # and again: still nothing consumed
+            r.read_application_data(out=memoryview(small))
+    big = mk(len(want) + 64)
+    pos = len(r.read_application_data(out=memoryview(big)))
+    assert bytes(big[:pos]) == b"".join(app[:20])
+    r.feed(b"".join(recs[20:]))
+    pos += len(r.read_application_data(out=memoryview(big)[pos:]))
+    assert bytes(big[:pos]) == want
+    with pytest.raises(TLSBadRecordMAC):
+        r.read_application_data(out=memoryview(big)[pos:])

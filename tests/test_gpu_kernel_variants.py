@@ -2,8 +2,6 @@
 up to 2048 records run one record per wavefront, larger ones a record per
 lane; each is forced here on ragged batches (lengths, alignment, AAD, tampered
 records) and checked bit-exact against the oracle."""
-import os
-
 import numpy as np
 import pytest
 
@@ -24,42 +22,23 @@ def tg(torch):
     return tlsgpu
 
 
-def _with_env(var, value):
-    class Ctx(object):
-        def __enter__(self):
-            self.old = os.environ.get(var)
-            os.environ[var] = value
-
-        def __exit__(self, *a):
-            if self.old is None:
-                del os.environ[var]
-            else:
-                os.environ[var] = self.old
-    return Ctx()
-
-
 LENS = [0, 1, 15, 16, 17, 63, 64, 65, 1000, 1024, 1040, 4095, 16383, 16384, 16385, 16400]
 
 
-@pytest.mark.parametrize("alg,klen,var,value", [
-    ("aesgcm", 16, "TLSGPU_GCM_VARIANT", "5"),          # lane per record, full rounds
-    ("aesgcm", 32, "TLSGPU_GCM_VARIANT", "5"),
-    ("aesgcm", 16, "TLSGPU_GCM_VARIANT", "7"),          # lane per record, counter windows
-    ("aesgcm", 32, "TLSGPU_GCM_VARIANT", "7"),
-    ("aesgcm", 16, "TLSGPU_GCM_VARIANT", "8"),          # windows, two blocks per group
-    ("aesgcm", 32, "TLSGPU_GCM_VARIANT", "9"),          # windows, rotated GHASH tables
-    ("aesgcm", 16, "TLSGPU_GCM_VARIANT", "13"),         # windows, three blocks per group
-    ("aesgcm", 16, "TLSGPU_GCM_VARIANT", "6"),          # wave per record
-    ("aesgcm", 32, "TLSGPU_GCM_VARIANT", "6"),
-    ("aesgcm", 16, "TLSGPU_GCM_VARIANT", "14"),         # 8-block bitsliced, octet per record
-    ("aesgcm", 32, "TLSGPU_GCM_VARIANT", "14"),
-    ("aesgcm", 16, "TLSGPU_GCM_VARIANT", "15"),         # hybrid T-table + bitsliced (persistent)
-    ("aesgcm", 32, "TLSGPU_GCM_VARIANT", "15"),
-    ("chacha", 32, "TLSGPU_CHACHA_VARIANT", "4"),       # lane per record
-    ("chacha", 32, "TLSGPU_CHACHA_VARIANT", "3"),       # wave per record
+@pytest.mark.parametrize("alg,klen,opt,value", [
+    ("aesgcm", 16, "gcm_variant", 16),          # T-table lane per record
+    ("aesgcm", 32, "gcm_variant", 16),
+    ("aesgcm", 16, "gcm_variant", 6),           # wave per record
+    ("aesgcm", 32, "gcm_variant", 6),
+    ("aesgcm", 16, "gcm_variant", 14),          # 8-block bitsliced, octet per record
+    ("aesgcm", 32, "gcm_variant", 14),
+    ("aesgcm", 16, "gcm_variant", 15),          # hybrid T-table + bitsliced (persistent)
+    ("aesgcm", 32, "gcm_variant", 15),
+    ("chacha", 32, "chacha_variant", 4),        # lane per record
+    ("chacha", 32, "chacha_variant", 3),        # wave per record
 ])
 @pytest.mark.parametrize("align", [16, 1])
-def test_forced_kernel_vs_oracle(torch, tg, oracle_mod, alg, klen, var, value, align):
+def test_forced_kernel_vs_oracle(torch, tg, oracle_mod, alg, klen, opt, value, align):
     from batchpack import HostBatch, run_seal_open
     rng = np.random.default_rng(hash((alg, klen, value, align)) & 0xffff)
     # + long records: many 256-counter windows (window-cache refreshes)
@@ -67,24 +46,22 @@ def test_forced_kernel_vs_oracle(torch, tg, oracle_mod, alg, klen, var, value, a
     hb = HostBatch(lens, payload_seed=align + 21, align=align, aad_mode="random")
     key = rng.bytes(klen)
     obj = tg.HipAESGCM(bytearray(key)) if alg == "aesgcm" else tg.HipCHACHA20_POLY1305(bytearray(key))
-    with _with_env(var, value):
+    with tg.options(**{opt: value}):
         run_seal_open(torch, tg, oracle_mod, hb, alg, np.frombuffer(key, np.uint8), obj,
                       tamper=(1, 30, 111))
 
 
-@pytest.mark.parametrize("keys", ["0", "1", "2"])   # LDS / scalar loads / row layout (default 4: folded)
-@pytest.mark.parametrize("klen", [16, 32])
-def test_hybrid_key_plane_sources(torch, tg, oracle_mod, keys, klen, monkeypatch):
-    """The hybrid kernel's alternative key-plane providers (TLSGPU_HY_KEYS)."""
-    from batchpack import HostBatch, run_seal_open
-    rng = np.random.default_rng(300 + klen + int(keys))
-    lens = LENS * 3 + list(rng.integers(0, 16401, 60)) + [65536, 70001]
-    hb = HostBatch(lens, payload_seed=31, align=16, aad_mode="random")
-    key = rng.bytes(klen)
-    monkeypatch.setenv("TLSGPU_GCM_VARIANT", "15")
-    monkeypatch.setenv("TLSGPU_HY_KEYS", keys)
-    run_seal_open(torch, tg, oracle_mod, hb, "aesgcm", np.frombuffer(key, np.uint8),
-                  tg.HipAESGCM(bytearray(key)), tamper=(2, 40))
+def test_unknown_variant_is_an_error(torch, tg):
+    """A variant no launcher knows fails the launch instead of running auto."""
+    from batchpack import HostBatch
+    hb = HostBatch([100, 200], payload_seed=1)
+    d = hb.to_device(torch)
+    obj = tg.HipAESGCM(bytearray(16))
+    with tg.options(gcm_variant=4):   # round 2's removed 32-block bitsliced kernel
+        with pytest.raises(tg.TlsGpuError):
+            tg.seal_batch(obj, hb.batch_kwargs(d))
+    with pytest.raises(tg.TlsGpuError):
+        tg.set_option("no_such_option", 1)
 
 
 @pytest.mark.parametrize("alg,klen", [("aesgcm", 16), ("chacha", 32)])
@@ -100,18 +77,20 @@ def test_auto_wave_per_record_batch(torch, tg, oracle_mod, alg, klen):
                   tamper=(0, 2047))
 
 
-@pytest.mark.parametrize("alg,klen,keys,gcmv", [("aesgcm", 16, 1, "7"), ("aesgcm", 16, 1, "14"),
-                                               ("aesgcm", 16, 1, "15"), ("aesgcm", 32, 1, "15"),
-                                               ("chacha", 32, 1, None), ("aesgcm", 32, 29, None),
-                                               ("chacha", 32, 29, None)])
+@pytest.mark.parametrize("alg,klen,keys,opts", [
+    ("aesgcm", 16, 1, {"gcm_variant": 16}), ("aesgcm", 16, 1, {"gcm_variant": 14}),
+    ("aesgcm", 16, 1, {"gcm_variant": 15}), ("aesgcm", 32, 1, {"gcm_variant": 15}),
+    ("chacha", 32, 1, {"chacha_variant": 4}),
+    ("aesgcm", 32, 29, {"gcm_table_variant": 1}), ("aesgcm", 32, 29, {"gcm_table_variant": 0}),
+    ("aesgcm", 16, 29, {"gcm_table_variant": 14}), ("chacha", 32, 29, {})])
 @pytest.mark.parametrize("align", [16, 1])
-def test_planned_mixed_batch(torch, tg, oracle_mod, alg, klen, keys, gcmv, align):
-    """> 2048 records with per-record lengths on a lane-per-record kernel run
-    longest first (planner.hip): every record must still land in its own
-    output slot.  Single-key batches of this size run a wave per record by
-    default, so the lane kernel is forced for them."""
+def test_planned_mixed_batch(torch, tg, oracle_mod, alg, klen, keys, opts, align):
+    """> 2048 records with per-record lengths on a lane-per-record or octet
+    kernel run in a planned order (planner.hip): every record must still land
+    in its own output slot.  Single-key batches of this size run a wave per
+    record by default, so the other kernels are forced for them."""
     from batchpack import HostBatch, run_seal_open
-    rng = np.random.default_rng(1000 + klen + keys + align + int(gcmv or 0))
+    rng = np.random.default_rng(1000 + klen + keys + align + sum(opts.values()))
     lens = list(rng.integers(0, 3000, 5000)) + [16384, 16400, 0, 1] * 5
     hb = HostBatch(lens, payload_seed=align, align=align, aad_mode="tls12", key_count=keys)
     kb = [rng.bytes(klen) for _ in range(keys)]
@@ -119,12 +98,10 @@ def test_planned_mixed_batch(torch, tg, oracle_mod, alg, klen, keys, gcmv, align
         obj = tg.HipAESGCM(bytearray(kb[0])) if alg == "aesgcm" else \
             tg.HipCHACHA20_POLY1305(bytearray(kb[0]))
         karr = np.frombuffer(kb[0], np.uint8)
-        env = ("TLSGPU_GCM_VARIANT", gcmv) if alg == "aesgcm" else ("TLSGPU_CHACHA_VARIANT", "4")
     else:
         obj = tg.KeyTable("chacha20-poly1305" if alg == "chacha" else "aesgcm", kb)
         karr = np.frombuffer(b"".join(kb), np.uint8).reshape(keys, klen)
-        env = ("TLSGPU_GCM_TABLE_VARIANT", "0")   # AES: the lane kernel
-    with _with_env(*env):
+    with tg.options(**opts):
         run_seal_open(torch, tg, oracle_mod, hb, alg, karr, obj, tamper=(7, 2500, 5019))
 
 
@@ -155,59 +132,116 @@ def test_auto_mixed_batch_wave_path(torch, tg, oracle_mod, alg, klen):
 
 
 @pytest.mark.parametrize("alg,klen", [("aesgcm", 16), ("aesgcm", 32), ("chacha", 32)])
-@pytest.mark.parametrize("waves", ["1", "4", "16"])
+@pytest.mark.parametrize("waves", [1, 4, 16])
 @pytest.mark.parametrize("align", [16, 1])
 def test_waves_per_record_forced(torch, tg, oracle_mod, alg, klen, waves, align):
-    """The wave-per-record kernels with one or four waves per record
-    (TLSGPU_WAVES_PER_RECORD; auto picks 16 / 4 / 1 by batch size):
-    the segment count changes every record's split point and H / r power."""
+    """The wave-per-record kernels with one, four or sixteen waves per record
+    (option waves_per_record; auto picks 16 / 4 / 1 by batch size): the
+    segment count changes every record's split point and H / r power."""
     from batchpack import HostBatch, run_seal_open
-    rng = np.random.default_rng(int(waves) * 100 + klen + align)
+    rng = np.random.default_rng(waves * 100 + klen + align)
     lens = LENS * 3 + list(rng.integers(0, 16401, 60)) + [20000, 65000]
     hb = HostBatch(lens, payload_seed=align + 40, align=align, aad_mode="random")
     key = rng.bytes(klen)
     obj = tg.HipAESGCM(bytearray(key)) if alg == "aesgcm" else tg.HipCHACHA20_POLY1305(bytearray(key))
-    var = "TLSGPU_GCM_VARIANT" if alg == "aesgcm" else "TLSGPU_CHACHA_VARIANT"
-    with _with_env(var, "6" if alg == "aesgcm" else "3"), \
-            _with_env("TLSGPU_WAVES_PER_RECORD", waves):
+    kind = {"gcm_variant": 6} if alg == "aesgcm" else {"chacha_variant": 3}
+    with tg.options(waves_per_record=waves, **kind):
         run_seal_open(torch, tg, oracle_mod, hb, alg, np.frombuffer(key, np.uint8), obj,
                       tamper=(2, 50, len(lens) - 1))
 
 
 @pytest.mark.parametrize("klen", [16, 32])
-@pytest.mark.parametrize("threads", ["512", "768", "1024"])
 @pytest.mark.parametrize("align", [16, 1])
-def test_key_table_wave_kernel(torch, tg, oracle_mod, klen, threads, align):
+def test_key_table_wave_kernel(torch, tg, oracle_mod, klen, align):
     """Many keys, mixed lengths, one wave per record (gcm_table_wave_kernel,
-    key-table variant 5): round keys from the record's key, GHASH powers from
+    gcm_table_variant 5): round keys from the record's key, GHASH powers from
     the key's precomputed table."""
     from batchpack import HostBatch, run_seal_open
-    rng = np.random.default_rng(300 + klen + int(threads) + align)
+    rng = np.random.default_rng(300 + klen + align)
     lens = LENS * 4 + list(rng.integers(0, 16401, 300)) + [20000, 65000]
     keys = 37
     hb = HostBatch(lens, payload_seed=align + 77, align=align, aad_mode="random", key_count=keys)
     kb = [rng.bytes(klen) for _ in range(keys)]
     obj = tg.KeyTable("aesgcm", kb)
     karr = np.frombuffer(b"".join(kb), np.uint8).reshape(keys, klen)
-    with _with_env("TLSGPU_GCM_TABLE_WAVE_THREADS", threads), \
-            _with_env("TLSGPU_GCM_TABLE_VARIANT", "5"):
+    with tg.options(gcm_table_variant=5):
         run_seal_open(torch, tg, oracle_mod, hb, "aesgcm", karr, obj, tamper=(4, 100, len(lens) - 1))
 
 
 @pytest.mark.parametrize("klen", [16, 32])
 @pytest.mark.parametrize("keys", [2, 37, 300])
 @pytest.mark.parametrize("align", [16, 1])
-def test_key_table_octet_kernel(torch, tg, oracle_mod, klen, keys, align, monkeypatch):
+@pytest.mark.parametrize("variant,split", [(14, 0), (0, 0), (0, 1000), (0, 4097)])
+def test_key_table_octet_kernel(torch, tg, oracle_mod, klen, keys, align, variant, split):
     """Many keys, ragged lengths, through the key-grouped octet kernel
-    (aes_gcm_bs8.hip gcm_kt_kernel, TLSGPU_GCM_TABLE_VARIANT=14): jobs of at
-    most eight records of one key, bitsliced keystream with the key's planes,
-    GHASH through the wave's 4-bit tables of the key's H^8."""
+    (aes_gcm_bs8.hip gcm_kt_kernel): jobs of at most eight records of one
+    key, bitsliced keystream with the key's planes, GHASH through the wave's
+    4-bit tables of the key's H^8.  Variant 14 sends every record there; the
+    auto path (0) splits the batch by length at kt_split (0 = the default
+    2048) and runs the shorter records through the lane kernel from the
+    tail of the same plan."""
     from batchpack import HostBatch, run_seal_open
-    rng = np.random.default_rng(700 + klen + keys + align)
-    lens = LENS * 4 + list(rng.integers(0, 16401, 400)) + [20000, 65000, 70001]
+    rng = np.random.default_rng(700 + klen + keys + align + split)
+    lens = LENS * 4 + list(rng.integers(0, 16401, 400)) + [999, 1000, 1001, 2047, 2048, 2049,
+                                                            4096, 4097, 20000, 65000, 70001]
     hb = HostBatch(lens, payload_seed=align + 91, align=align, aad_mode="random", key_count=keys)
     kb = [rng.bytes(klen) for _ in range(keys)]
     obj = tg.KeyTable("aesgcm", kb)
     karr = np.frombuffer(b"".join(kb), np.uint8).reshape(keys, klen)
-    monkeypatch.setenv("TLSGPU_GCM_TABLE_VARIANT", "14")
-    run_seal_open(torch, tg, oracle_mod, hb, "aesgcm", karr, obj, tamper=(4, 100, len(lens) - 1))
+    with tg.options(gcm_table_variant=variant, kt_split=split):
+        run_seal_open(torch, tg, oracle_mod, hb, "aesgcm", karr, obj, tamper=(4, 100, len(lens) - 1))
+
+
+@pytest.mark.parametrize("alg,opts", [("aesgcm", {"gcm_table_variant": 0}),
+                                      ("aesgcm", {"gcm_table_variant": 1}),
+                                      ("aesgcm", {"gcm_table_variant": 5}),
+                                      ("aesgcm", {"gcm_table_variant": 14}),
+                                      ("chacha", {}), ("aesccm", {"ccm_variant": 2}),
+                                      ("aesccm", {"ccm_variant": 3})])
+def test_key_index_out_of_range_is_skipped(torch, tg, oracle_mod, alg, opts):
+    """A key-table record whose key_idx is not below the table's size is
+    never read past the table: seal leaves its output alone, open reports
+    status 0; every other record is sealed and opened as usual."""
+    from batchpack import HostBatch
+    nk = 7
+    rng = np.random.default_rng(55)
+    lens = list(rng.integers(0, 5000, 3000)) + [16384] * 40
+    hb = HostBatch(lens, payload_seed=3, align=16, aad_mode="tls12", key_count=nk)
+    bad = np.array([0, 5, 17, 1500, 2999, 3020], dtype=np.int64)
+    hb.key_idx[bad] = np.array([nk, nk + 1, 0xffffffff, nk, 1000, nk], dtype=np.uint32)
+    klen = 32 if alg == "chacha" else 16
+    kb = [rng.bytes(klen) for _ in range(nk)]
+    name = {"aesgcm": "aesgcm", "chacha": "chacha20-poly1305", "aesccm": "aesccm"}[alg]
+    table = tg.KeyTable(name, kb)
+    karr = np.frombuffer(b"".join(kb), np.uint8).reshape(nk, klen)
+    good = np.setdiff1d(np.arange(hb.n), bad)
+    with tg.options(**opts):
+        d = hb.to_device(torch)
+        tg.seal_batch(table, hb.batch_kwargs(d))
+        torch.cuda.synchronize()
+        got = d["out"].cpu().numpy()
+        kidx = hb.key_idx.copy()
+        hb.key_idx = np.where(kidx < nk, kidx, 0).astype(np.uint32)   # the oracle needs valid keys
+        want, _ = hb.oracle(oracle_mod, alg, karr, "seal")
+        hb.key_idx = kidx
+        for i in good:
+            o, L = int(hb.out_off[i]), int(hb.lens[i])
+            assert np.array_equal(got[o:o + L + 16], want[o:o + L + 16]), ("seal", i)
+        for i in bad:
+            o, L = int(hb.out_off[i]), int(hb.lens[i])
+            assert not got[o:o + L + 16].any(), ("skipped record written", i)
+        # open: the good records' sealed bytes back, bad ones rejected
+        src = d["out"].clone()
+        pt = torch.zeros(hb.in_bytes, dtype=torch.uint8, device="cuda")
+        status = torch.full((hb.n,), 7, dtype=torch.uint8, device="cuda")
+        tg.open_batch(table, tg.make_batch(hb.n, src, pt, d["nonces"], aad=d["aad"], lens=d["lens"],
+                                           in_off=d["out_off"], out_off=d["in_off"], aad_off=d["aad_off"],
+                                           aad_len=d["aad_len"], key_idx=d["key_idx"], status=status))
+        torch.cuda.synchronize()
+        st = status.cpu().numpy()
+        assert (st[bad] == 0).all()
+        assert (st[good] == 1).all()
+        back = pt.cpu().numpy()
+        for i in good[::37]:
+            o, L = int(hb.in_off[i]), int(hb.lens[i])
+            assert np.array_equal(back[o:o + L], hb.inp[o:o + L]), ("open", i)

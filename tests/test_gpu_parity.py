@@ -185,13 +185,17 @@ def test_config1_digest(torch, tg):
 # ------------------------------------------- full-size (BASELINE configs 2/3)
 
 @pytest.mark.parametrize("alg", ["aesgcm", "chacha", "aesgcm-bs8"])
-def test_full_size_roundtrip_and_samples(torch, tg, oracle_mod, alg, monkeypatch):
+def test_full_size_roundtrip_and_samples(torch, tg, oracle_mod, alg):
     """2^20 x 16 KiB records: seal -> open round trip on the whole batch
     (size-independent property), and 64 sampled records bit-exact vs the oracle.
-    aesgcm-bs8 forces the 8-block bitsliced kernel (TLSGPU_GCM_VARIANT=14)."""
-    if alg == "aesgcm-bs8":
-        monkeypatch.setenv("TLSGPU_GCM_VARIANT", "14")
-        alg = "aesgcm"
+    aesgcm-bs8 forces the 8-block bitsliced kernel (gcm_variant 14)."""
+    variant = 14 if alg == "aesgcm-bs8" else 0
+    alg = "aesgcm" if alg == "aesgcm-bs8" else alg
+    with tg.options(gcm_variant=variant):
+        _full_size(torch, tg, oracle_mod, alg)
+
+
+def _full_size(torch, tg, oracle_mod, alg):
     n, L = 1 << 20, 16384
     g = torch.Generator(device="cuda").manual_seed(0x7715)
     inp = torch.randint(0, 256, (n * L,), dtype=torch.uint8, device="cuda", generator=g)

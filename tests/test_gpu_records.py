@@ -188,3 +188,52 @@ def test_record_limits_device(torch, tg):
     wires, opened = _run(torch, tg, "tls12", "aes128gcm", key, iv[:4], 9, [23, 23],
                          [bytes(16385), bytes(16384)], [0, 0], True)
     assert [o[0] for o in opened] == [7, 0]
+
+
+@pytest.mark.parametrize("n", [32768, 1 << 20])
+def test_config5_full_shape_vs_oracle(torch, tg, n):
+    """BASELINE configs[4] through the path bench.py --config c5 runs:
+    tg_seal_records on n TLS 1.3 AES-128-GCM records of 16 384 application
+    bytes (inner plaintext 16 385 = 64 q + 1 blocks: the hybrid kernel's
+    one-block last batch), bench.py's layout (header at 128 k + 123, so the
+    ciphertext starts on a 128-byte line), seq0 far from 0.  n >= 32 768 runs
+    the hybrid octet kernel.  128 sampled wire records -- the first and the
+    last among them -- equal the framing oracle's (recordlayer.py:592-641,
+    :536-565 restated, pinned to the reference RecordLayer); every record
+    opens back with status ok, content type 0x17 and its fragment."""
+    import bench
+    from oracle import records as R
+    L = bench.C5_APP
+    DS, WS, H = bench.c5_layout(L)
+    seq0 = 2 ** 40 + 12345
+    key, iv = bytes(detbytes("c5-key", 16)), bytes(detbytes("c5-iv", 12))
+    g = torch.Generator(device="cuda").manual_seed(0xc5)
+    data = torch.randint(0, 256, (n * DS,), dtype=torch.uint8, device="cuda", generator=g)
+    orig = data.view(n, DS)[:, :L].clone()
+    data_off = torch.arange(n, dtype=torch.int64, device="cuda") * DS
+    data_len = torch.full((n,), L, dtype=torch.int32, device="cuda")
+    ctype = torch.full((n,), 0x17, dtype=torch.uint8, device="cuda")
+    wire_off = torch.arange(n, dtype=torch.int64, device="cuda") * WS + H
+    wire = torch.zeros(n * WS, dtype=torch.uint8, device="cuda")
+    wire_len = torch.zeros(n, dtype=torch.int32, device="cuda")
+    k = tg.HipAESGCM(bytearray(key))
+    tg.seal_records(k, tg.TLS13, iv, seq0, n, data, data_off, data_len, ctype, wire, wire_off,
+                    wire_len)
+    torch.cuda.synchronize()
+    assert bool((wire_len == 5 + L + 1 + 16).all())
+    samples = bench.c5_samples(data, wire, wire_len, bench.c5_pick(n), L)
+    assert samples[0][0] == 0 and samples[-1][0] == n - 1 and len(samples) == 128
+    for i, frag, w in samples:
+        assert frag == orig[i].cpu().numpy().tobytes()
+        assert w == R.seal_record("tls13", "aes128gcm", key, iv, seq0 + i, 0x17, frag), i
+    back = torch.zeros(n * DS, dtype=torch.uint8, device="cuda")
+    o_len = torch.zeros(n, dtype=torch.int32, device="cuda")
+    o_ct = torch.zeros(n, dtype=torch.uint8, device="cuda")
+    st = torch.full((n,), 255, dtype=torch.uint8, device="cuda")
+    tg.open_records(k, tg.TLS13, iv, seq0, n, wire, wire_off, wire_len, back, data_off, o_len, o_ct, st)
+    torch.cuda.synchronize()
+    assert int((st == 0).sum()) == n
+    assert bool((o_ct == 0x17).all()) and bool((o_len == L).all())
+    assert torch.equal(back.view(n, DS)[:, :L], orig)
+    del data, orig, wire, back
+    torch.cuda.empty_cache()

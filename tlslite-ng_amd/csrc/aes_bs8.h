@@ -6,7 +6,7 @@
 // waves per SIMD:
 //   * s[i][b] = bit plane b of state row i: byte c of the register is column
 //     c, bit j of that byte is block j of the lane's eight blocks;
-//   * SubBytes is the same 84-gate Boyar-Peralta circuit as aes_bs.h (one
+//   * SubBytes is the 72-gate Boyar-Peralta cover of aes_bs.h (one
 //     call covers the four bytes of a row for all eight blocks), its 0x63
 //     folded into the next round key;
 //   * ShiftRows rotates row i right by i bytes (one v_alignbit per plane);

@@ -28,6 +28,7 @@
 #include <stdlib.h>
 
 #include "aes_round.h"
+#include "options.h"
 
 namespace tg {
 namespace {
@@ -151,14 +152,19 @@ __device__ __forceinline__ void ccm_record(const tg_batch& b, uint64_t i, uint32
 }
 
 // WIN: the keystream through the 256-counter window cache (default);
-// TLSGPU_CCM_VARIANT=1 runs full rounds (measurement).
+// option ccm_variant 1 runs full rounds (measurement).  A key-table record
+// whose key_idx is not below nkeys is skipped (open: status 0).
 template <int NR, bool OPEN, int TAG, bool TABLE, bool WIN>
 __global__ __launch_bounds__(ccm_threads<TABLE>()) void ccm_kernel(const AesKeyDev* __restrict__ keys,
-                                                          tg_batch b) {
+                                                          uint64_t nkeys, tg_batch b) {
     stage_te(reinterpret_cast<uint32_t*>(g_lds_ccm));   // Te0/Te2 copies at LDS 0
     __syncthreads();
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= b.n) return;
+    if (TABLE && b.key_idx[i] >= nkeys) {
+        if (OPEN && b.status) b.status[i] = 0;
+        return;
+    }
     const AesKeyDev* kp = TABLE ? keys + b.key_idx[i] : keys;
     RkRegs<NR> rk;
 #pragma unroll
@@ -276,9 +282,13 @@ constexpr size_t kCcmWaveLds = 65536 + 2048 + 32 + 240;
 
 template <int NR, bool OPEN, int TAG, bool TABLE>
 __global__ __launch_bounds__(kCcmWaveThreads) void ccm_wave_kernel(const AesKeyDev* __restrict__ keys,
-                                                                   tg_batch b) {
-    stage_quad(g_lds_ccm);
+                                                                   uint64_t nkeys, tg_batch b) {
     const uint64_t i = blockIdx.x;                 // the record (workgroup-uniform)
+    if (TABLE && b.key_idx[i] >= nkeys) {          // out-of-range key index: skipped
+        if (OPEN && b.status && threadIdx.x == 0) b.status[i] = 0;
+        return;
+    }
+    stage_quad(g_lds_ccm);
     const AesKeyDev* kp = TABLE ? keys + b.key_idx[i] : keys;
     uint32_t* rkw = reinterpret_cast<uint32_t*>(reinterpret_cast<uint8_t*>(g_lds_ccm) + kCcmRk);
     if (threadIdx.x < 4 * (NR + 1)) rkw[threadIdx.x] = kp->rk[threadIdx.x];
@@ -376,17 +386,11 @@ __global__ __launch_bounds__(kCcmWaveThreads) void ccm_wave_kernel(const AesKeyD
 }
 
 template <int NR, bool OPEN, int TAG, bool TABLE>
-int launch_wave(const AesKeyDev* keys, const tg_batch& b, hipStream_t s) {
-    static bool attr_set = false;
-    if (!attr_set) {
-        if (hipFuncSetAttribute((const void*)ccm_wave_kernel<NR, OPEN, TAG, TABLE>,
-                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)kCcmWaveLds) !=
-            hipSuccess)
-            return TG_EHIP;
-        attr_set = true;
-    }
+int launch_wave(const AesKeyDev* keys, uint64_t nkeys, const tg_batch& b, hipStream_t s) {
+    if (lds_attr((const void*)ccm_wave_kernel<NR, OPEN, TAG, TABLE>, (int)kCcmWaveLds)) return TG_EHIP;
+    if (b.n > 0x7fffffffull) return TG_EINVAL;
     hipLaunchKernelGGL((ccm_wave_kernel<NR, OPEN, TAG, TABLE>), dim3((unsigned)b.n),
-                       dim3(kCcmWaveThreads), kCcmWaveLds, s, keys, b);
+                       dim3(kCcmWaveThreads), kCcmWaveLds, s, keys, nkeys, b);
     return hipGetLastError() == hipSuccess ? TG_OK : TG_EHIP;
 }
 
@@ -396,57 +400,56 @@ int launch_wave(const AesKeyDev* keys, const tg_batch& b, hipStream_t s) {
 constexpr uint64_t kCcmWaveMaxRecords = 4096;
 
 template <int NR, bool OPEN, int TAG, bool TABLE, bool WIN>
-int launch_w(const AesKeyDev* keys, const tg_batch& b, hipStream_t s) {
-    static bool attr_set = false;
-    if (!attr_set) {
-        if (hipFuncSetAttribute((const void*)ccm_kernel<NR, OPEN, TAG, TABLE, WIN>,
-                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)kCcmLds) !=
-            hipSuccess)
-            return TG_EHIP;
-        attr_set = true;
-    }
+int launch_w(const AesKeyDev* keys, uint64_t nkeys, const tg_batch& b, hipStream_t s) {
+    if (lds_attr((const void*)ccm_kernel<NR, OPEN, TAG, TABLE, WIN>, (int)kCcmLds)) return TG_EHIP;
     constexpr int threads = ccm_threads<TABLE>();
     const uint64_t blocks = (b.n + threads - 1) / threads;
+    if (blocks > 0x7fffffffull) return TG_EINVAL;
     hipLaunchKernelGGL((ccm_kernel<NR, OPEN, TAG, TABLE, WIN>), dim3((unsigned)blocks),
-                       dim3(threads), kCcmLds, s, keys, b);
+                       dim3(threads), kCcmLds, s, keys, nkeys, b);
     return hipGetLastError() == hipSuccess ? TG_OK : TG_EHIP;
 }
 
-// TLSGPU_CCM_VARIANT (read per launch; tests and measurement): 0 = auto (wave
-// per record up to kCcmWaveMaxRecords, else lane per record with the window
-// cache), 1 = lane per record, full rounds, 2 = wave per record, 3 = lane per
-// record with the window cache.
+// Option ccm_variant (tests and measurement): 0 = auto (wave per record up
+// to kCcmWaveMaxRecords, else lane per record with the window cache), 1 =
+// lane per record, full rounds, 2 = wave per record, 3 = lane per record
+// with the window cache.
 template <int NR, bool OPEN, int TAG, bool TABLE>
-int launch(const AesKeyDev* keys, const tg_batch& b, hipStream_t s) {
-    const char* e = getenv("TLSGPU_CCM_VARIANT");
-    const int v = e ? atoi(e) : 0;
-    if (v == 1) return launch_w<NR, OPEN, TAG, TABLE, false>(keys, b, s);
-    if (v == 2 || (v == 0 && b.n <= kCcmWaveMaxRecords)) return launch_wave<NR, OPEN, TAG, TABLE>(keys, b, s);
-    return launch_w<NR, OPEN, TAG, TABLE, true>(keys, b, s);
+int launch(const AesKeyDev* keys, uint64_t nkeys, const tg_batch& b, hipStream_t s) {
+    switch (opt(kOptCcmVariant)) {
+        case 0:
+            if (b.n <= kCcmWaveMaxRecords) return launch_wave<NR, OPEN, TAG, TABLE>(keys, nkeys, b, s);
+            return launch_w<NR, OPEN, TAG, TABLE, true>(keys, nkeys, b, s);
+        case 1: return launch_w<NR, OPEN, TAG, TABLE, false>(keys, nkeys, b, s);
+        case 2: return launch_wave<NR, OPEN, TAG, TABLE>(keys, nkeys, b, s);
+        case 3: return launch_w<NR, OPEN, TAG, TABLE, true>(keys, nkeys, b, s);
+        default: return TG_EINVAL;
+    }
 }
 
 template <int NR, int TAG, bool TABLE>
-int launch_op(const AesKeyDev* keys, const tg_batch& b, bool open, hipStream_t s) {
-    return open ? launch<NR, true, TAG, TABLE>(keys, b, s) : launch<NR, false, TAG, TABLE>(keys, b, s);
+int launch_op(const AesKeyDev* keys, uint64_t nkeys, const tg_batch& b, bool open, hipStream_t s) {
+    return open ? launch<NR, true, TAG, TABLE>(keys, nkeys, b, s) : launch<NR, false, TAG, TABLE>(keys, nkeys, b, s);
 }
 
 template <int NR, bool TABLE>
-int launch_tag(const AesKeyDev* keys, int taglen, const tg_batch& b, bool open, hipStream_t s) {
-    return taglen == 16 ? launch_op<NR, 16, TABLE>(keys, b, open, s)
-                        : launch_op<NR, 8, TABLE>(keys, b, open, s);
+int launch_tag(const AesKeyDev* keys, uint64_t nkeys, int taglen, const tg_batch& b, bool open, hipStream_t s) {
+    return taglen == 16 ? launch_op<NR, 16, TABLE>(keys, nkeys, b, open, s)
+                        : launch_op<NR, 8, TABLE>(keys, nkeys, b, open, s);
 }
 
 }  // namespace
 }  // namespace tg
 
-int tg_launch_ccm(const tg::AesKeyDev* keys, bool table, int rounds, int taglen,
+int tg_launch_ccm(const tg::AesKeyDev* keys, uint64_t nkeys, int rounds, int taglen,
                   const tg_batch& b, bool open, hipStream_t s) {
     if (taglen != 16 && taglen != 8) return TG_EINVAL;
+    const bool table = nkeys > 1;
     if (rounds == 10)
-        return table ? tg::launch_tag<10, true>(keys, taglen, b, open, s)
-                     : tg::launch_tag<10, false>(keys, taglen, b, open, s);
+        return table ? tg::launch_tag<10, true>(keys, nkeys, taglen, b, open, s)
+                     : tg::launch_tag<10, false>(keys, nkeys, taglen, b, open, s);
     if (rounds == 14)
-        return table ? tg::launch_tag<14, true>(keys, taglen, b, open, s)
-                     : tg::launch_tag<14, false>(keys, taglen, b, open, s);
+        return table ? tg::launch_tag<14, true>(keys, nkeys, taglen, b, open, s)
+                     : tg::launch_tag<14, false>(keys, nkeys, taglen, b, open, s);
     return TG_EINVAL;
 }

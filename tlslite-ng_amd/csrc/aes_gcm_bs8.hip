@@ -31,6 +31,7 @@
 #include "aes_bs8.h"
 #include "aes_round.h"
 #include "ghash.h"
+#include "options.h"
 
 namespace tg {
 namespace {
@@ -154,7 +155,7 @@ struct TableKeyCtx {    // a key of a key table: the wave's 4-bit H^8 tables in 
 // T-table cipher (aes_round.h, Te tables at kTeBase, round keys in SGPRs)
 // instead of the bitsliced one; everything else is shared.  ``recb``: this
 // wave's 1 KiB of LDS for the records' first-state planes.
-template <int NR, bool OPEN, bool TROLE, class KM, class KC>
+template <int NR, bool OPEN, bool TROLE, class KM, class KC, bool PRE = false>
 __device__ __forceinline__ void octet_job(const KC& kc, const tg_batch& b,
                                           const uint32_t* __restrict__ order, uint64_t t0,
                                           uint32_t recw, const RkLds& rkT, uint32_t sbox,
@@ -308,14 +309,22 @@ __device__ __forceinline__ void octet_job(const KC& kc, const tg_batch& b,
             for (int bb = 0; bb < 6; ++bb) s[3][bb] ^= lanec[bb];
             bs8::ctr_planes<6, 16>(s, kmask, beta);
             if ((beta + 1u) >> 10) bs8::ctr_planes<16, 32>(s, kmask, beta);
+            // PRE: the batch's payload is loaded before the cipher runs, so
+            // the XOR does not wait for HBM (32 VGPRs live across encrypt():
+            // only at three waves per SIMD; at four the seal kernel spilled
+            // 270 registers)
+            uint4 dp[8];
+            const bool pre = PRE && blk0 < (nfast << 6);
+            if (pre && valid) {
+#pragma unroll
+                for (int q = 0; q < 8; ++q) dp[q] = gload16u(in + 16u * (blk0 + 8u * q));
+            }
             uint32_t w[4][8];
             bs8::encrypt<NR>(s, km, w);
             uint4 ks[8];
 #pragma unroll
             for (int j = 0; j < 8; ++j) ks[j] = make_uint4(w[0][j], w[1][j], w[2][j], w[3][j]);
-            // (loading the payload before encrypt() too would keep 32 more
-            // VGPRs live across it: 270 spilled registers in the seal kernel)
-            consume(ks, blk0, 0, std::integral_constant<int, 8>(), nullptr);
+            consume(ks, blk0, 0, std::integral_constant<int, 8>(), pre ? dp : nullptr);
         }
     }
     if (!__any(valid)) return;
@@ -388,22 +397,27 @@ __global__ __launch_bounds__(kBs8Threads, 4) void gcm_bs8_kernel(const GcmKeyDev
 // so the LDS and the VALU are busy at the same time.
 // LDS: H^8 tables [0, 64K), Te0/Te2 copies [64K, 128K), S-box, then 1 KiB of
 // record planes per wave.
+// 1024 threads = 16 waves = 4 per SIMD at <= 128 VGPRs; 768 = 3 per SIMD
+// at <= 168 VGPRs, which lets the bitsliced waves prefetch their payload
+// (option hy_threads).
 constexpr int kHyThreads = 1024;
 constexpr uint32_t kHySbox = 2 * 65536;
 constexpr uint32_t kHyRk = kHySbox + 256;               // 15 round keys (16 B each)
 constexpr uint32_t kHyJt = kHyRk + 256;                 // gmul_rot lane-offset rows
 constexpr uint32_t kHyKeys = kHyJt + 256;               // round-key planes (bs8::KeyPlanesLds)
 constexpr uint32_t kHyRecBase = kHyKeys + 2048;
-constexpr size_t kHyLds = kHyRecBase + (kHyThreads / 64) * 1024;
+constexpr size_t kHyLds = kHyRecBase + (kHyThreads / 64) * 1024;   // for either size
 static_assert(kTeBase == 65536, "Te block follows the GHASH tables");
 
 // The batch descriptor is read from memory per job (bp): held in SGPRs
 // across the persistent loop it would crowd out the ciphers' own scalars.
-// KEYS: where the bitsliced waves read the round-key planes -- 1 scalar loads
-// (SGPR operands), 0 LDS, 2 vector loads of the row layout at ``krows``
-// (VGPR operands without LDS traffic); TLSGPU_HY_KEYS selects.
-template <int NR, bool OPEN, int KEYS>
-__global__ __launch_bounds__(kHyThreads) void gcm_hy_kernel(const GcmKeyDev* __restrict__ key,
+// The bitsliced waves read the MixColumns-folded round-key planes from the
+// row layout at ``krows`` (compiler-scalarised loads: SGPR operands, 1.3 %
+// faster than the plain planes and 3 % faster than LDS-staged ones, whose
+// LDS reads compete with the T-table waves; profiles/r02/v58_fold_keys/,
+// v25_hy_keys.txt).
+template <int NR, bool OPEN, int THREADS>
+__global__ __launch_bounds__(THREADS) void gcm_hy_kernel(const GcmKeyDev* __restrict__ key,
                                                             const tg_batch* bp,
                                                             const uint32_t* __restrict__ order,
                                                             uint32_t* __restrict__ queue,
@@ -413,7 +427,6 @@ __global__ __launch_bounds__(kHyThreads) void gcm_hy_kernel(const GcmKeyDev* __r
     stage_te(reinterpret_cast<uint32_t*>(g_lds_bs8) + kTeBase / 4);
     stage_sbox(kHySbox);
     if (threadIdx.x < 4 * (NR + 1)) reinterpret_cast<uint32_t*>(g_lds_bs8)[kHyRk / 4 + threadIdx.x] = key->rk[threadIdx.x];
-    if (KEYS == 0) bs8::stage_lds_planes(kHyKeys, key->bs8mask, NR);
     __syncthreads();
     const uint32_t wave = (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
     const uint64_t njobs = (bp->n + 7) / 8;
@@ -430,7 +443,7 @@ __global__ __launch_bounds__(kHyThreads) void gcm_hy_kernel(const GcmKeyDev* __r
             asm volatile("" ::: "memory");
             const tg_batch b = *bp;
             octet_job<NR, OPEN, true>(SingleKeyRowCtx{key, jw}, b, order, 8ull * job, recw, rk,
-                                      kHySbox, bs8::KeyPlanesLds{kHyKeys});
+                                      kHySbox, bs8::KeyPlanesVmemFolded{{krows}});
         }
     } else {
         const RkLds none{0};
@@ -441,28 +454,19 @@ __global__ __launch_bounds__(kHyThreads) void gcm_hy_kernel(const GcmKeyDev* __r
             if (job >= njobs) break;
             asm volatile("" ::: "memory");
             const tg_batch b = *bp;
-            if (KEYS == 0)
-                octet_job<NR, OPEN, false>(SingleKeyRowCtx{key, jw}, b, order, 8ull * job, recw,
-                                           none, kHySbox, bs8::KeyPlanesLds{kHyKeys});
-            else if (KEYS == 2)
-                octet_job<NR, OPEN, false>(SingleKeyRowCtx{key, jw}, b, order, 8ull * job, recw,
-                                           none, kHySbox, bs8::KeyPlanesVmem{krows});
-            else if (KEYS == 4)
-                octet_job<NR, OPEN, false>(SingleKeyRowCtx{key, jw}, b, order, 8ull * job, recw,
-                                           none, kHySbox, bs8::KeyPlanesVmemFolded{{krows}});
-            else
-                octet_job<NR, OPEN, false>(SingleKeyRowCtx{key, jw}, b, order, 8ull * job, recw,
-                                           none, kHySbox, bs8::KeyPlanes{key->bs8mask});
+            octet_job<NR, OPEN, false, bs8::KeyPlanesVmemFolded, SingleKeyRowCtx, (THREADS < 1024)>(
+                SingleKeyRowCtx{key, jw}, b, order, 8ull * job, recw, none, kHySbox,
+                bs8::KeyPlanesVmemFolded{{krows}});
         }
     }
 }
 
 // Stream-ordered setup of the hybrid kernel's scratch: the job counter and a
 // device copy of the batch descriptor.
-// fold: the rows hold bs8_fold_word planes (KeyPlanesVmemFolded) for rounds
-// 1 .. nr - 1 instead of the round-key planes.
+// The rows hold the bs8_fold_word planes (KeyPlanesVmemFolded) for rounds
+// 1 .. nr - 1 and the round-key planes for rounds 0 and nr.
 __global__ void hy_setup_kernel(tg_batch b, uint32_t* queue, tg_batch* bcopy,
-                                const GcmKeyDev* __restrict__ key, uint32_t* krows, int nr, int fold) {
+                                const GcmKeyDev* __restrict__ key, uint32_t* krows, int nr) {
     if (threadIdx.x == 0) {
         *queue = 0;
         *bcopy = b;
@@ -470,19 +474,13 @@ __global__ void hy_setup_kernel(tg_batch b, uint32_t* queue, tg_batch* bcopy,
     for (int e = threadIdx.x; e < 32 * (nr + 1); e += blockDim.x) {   // KeyPlanesVmem layout
         const int r = e >> 5, i = (e >> 3) & 3, bit = e & 7;
         krows[4 * (8 * r + bit) + i] =
-            fold && r >= 1 && r < nr ? bs8_fold_word(key->rk, e) : key->bs8mask[e];
+            r >= 1 && r < nr ? bs8_fold_word(key->rk, e) : key->bs8mask[e];
     }
 }
 
 template <int NR, bool OPEN>
 int launch_bs8(const GcmKeyDev* key, const tg_batch& b, hipStream_t s, const uint32_t* order) {
-    static bool attr_set = false;
-    if (!attr_set) {
-        if (hipFuncSetAttribute((const void*)gcm_bs8_kernel<NR, OPEN>,
-                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)kBs8Lds) != hipSuccess)
-            return TG_EHIP;
-        attr_set = true;
-    }
+    if (lds_attr((const void*)gcm_bs8_kernel<NR, OPEN>, (int)kBs8Lds)) return TG_EHIP;
     const uint64_t groups = (b.n + kBs8Recs - 1) / kBs8Recs;
     if (groups > 0x7fffffffull) return TG_EINVAL;
     hipLaunchKernelGGL((gcm_bs8_kernel<NR, OPEN>), dim3((unsigned)groups), dim3(kBs8Threads), kBs8Lds, s,
@@ -490,55 +488,38 @@ int launch_bs8(const GcmKeyDev* key, const tg_batch& b, hipStream_t s, const uin
     return hipGetLastError() == hipSuccess ? TG_OK : TG_EHIP;
 }
 
-template <int NR, bool OPEN, int KEYS>
-int launch_hy_k(const GcmKeyDev* key, const tg_batch& b, hipStream_t s, const uint32_t* order,
-                uint32_t nt, uint32_t prio) {
-    static bool attr_set = false;
-    if (!attr_set) {
-        if (hipFuncSetAttribute((const void*)gcm_hy_kernel<NR, OPEN, KEYS>,
-                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)kHyLds) != hipSuccess)
-            return TG_EHIP;
-        attr_set = true;
-    }
-    // job counter + batch copy: stream-ordered scratch, so concurrent batches
-    // never share them
+// Options hy_t (T-table waves per 16, default 8) and hy_noprio (1: the
+// T-table waves keep normal priority) are measurement knobs.
+template <int NR, bool OPEN>
+int launch_hy(const GcmKeyDev* key, const tg_batch& b, hipStream_t s, const uint32_t* order) {
+    if ((b.n + 7) / 8 > 0xffffffffull) return TG_EINVAL;
+    const int t = opt(kOptHyT);
+    const bool small = opt(kOptHyThreads) == 768;
+    const int waves = small ? 12 : 16;
+    const uint32_t nt = t > 0 && t <= waves ? (uint32_t)t : (uint32_t)waves / 2;
+    const uint32_t prio = opt(kOptHyNoPrio) ? 0u : 1u;
+    const void* fn = small ? (const void*)gcm_hy_kernel<NR, OPEN, 768> : (const void*)gcm_hy_kernel<NR, OPEN, 1024>;
+    if (lds_attr(fn, (int)kHyLds)) return TG_EHIP;
+    // job counter + batch copy + key rows: stream-ordered scratch, so
+    // concurrent batches never share them
     uint8_t* scratch = nullptr;
     if (hipMallocAsync((void**)&scratch, 256 + 2048, s) != hipSuccess) return TG_EHIP;
     uint32_t* queue = reinterpret_cast<uint32_t*>(scratch);
     tg_batch* bcopy = reinterpret_cast<tg_batch*>(scratch + 64);
     uint32_t* krows = reinterpret_cast<uint32_t*>(scratch + 256);
-    hipLaunchKernelGGL(hy_setup_kernel, dim3(1), dim3(64), 0, s, b, queue, bcopy, key, krows, NR,
-                       KEYS == 4 ? 1 : 0);
+    hipLaunchKernelGGL(hy_setup_kernel, dim3(1), dim3(64), 0, s, b, queue, bcopy, key, krows, NR);
     bool ok = hipGetLastError() == hipSuccess;
     if (ok) {
-        hipLaunchKernelGGL((gcm_hy_kernel<NR, OPEN, KEYS>), dim3((unsigned)device_cus()), dim3(kHyThreads),
-                           kHyLds, s, key, (const tg_batch*)bcopy, order, queue, nt, prio,
-                           (const uint4*)krows);
+        if (small)
+            hipLaunchKernelGGL((gcm_hy_kernel<NR, OPEN, 768>), dim3((unsigned)device_cus()), dim3(768), kHyLds, s,
+                               key, (const tg_batch*)bcopy, order, queue, nt, prio, (const uint4*)krows);
+        else
+            hipLaunchKernelGGL((gcm_hy_kernel<NR, OPEN, 1024>), dim3((unsigned)device_cus()), dim3(1024), kHyLds,
+                               s, key, (const tg_batch*)bcopy, order, queue, nt, prio, (const uint4*)krows);
         ok = hipGetLastError() == hipSuccess;
     }
     if (hipFreeAsync(scratch, s) != hipSuccess) return TG_EHIP;
     return ok ? TG_OK : TG_EHIP;
-}
-
-// TLSGPU_HY_T (T-table waves per 16, default 8), TLSGPU_HY_PRIO (default 1)
-// and TLSGPU_HY_KEYS (4: the MixColumns-folded planes by scalar loads,
-// default, 1.3 % faster than 1, profiles/r02/v58_fold_keys/; 1: the round-key
-// planes by scalar loads; 0: from LDS, 2 % slower than 1 in the hybrid: the
-// T-table waves own the LDS, profiles/r02/v25_hy_keys.txt; 2: the row layout
-// by (compiler-scalarised) loads) are read per launch (measurement).
-template <int NR, bool OPEN>
-int launch_hy(const GcmKeyDev* key, const tg_batch& b, hipStream_t s, const uint32_t* order) {
-    if ((b.n + 7) / 8 > 0xffffffffull) return TG_EINVAL;
-    const char* et = getenv("TLSGPU_HY_T");
-    const char* ep = getenv("TLSGPU_HY_PRIO");
-    const char* ek = getenv("TLSGPU_HY_KEYS");
-    const uint32_t nt = et ? (uint32_t)atoi(et) : 8u;
-    const uint32_t prio = ep ? (uint32_t)atoi(ep) : 1u;
-    const int keys = ek ? atoi(ek) : 4;
-    if (keys == 0) return launch_hy_k<NR, OPEN, 0>(key, b, s, order, nt, prio);
-    if (keys == 2) return launch_hy_k<NR, OPEN, 2>(key, b, s, order, nt, prio);
-    if (keys == 4) return launch_hy_k<NR, OPEN, 4>(key, b, s, order, nt, prio);
-    return launch_hy_k<NR, OPEN, 1>(key, b, s, order, nt, prio);
 }
 
 // ---- key tables: key-grouped octet jobs on bitsliced waves ----------------
@@ -573,7 +554,8 @@ __global__ __launch_bounds__(kKtThreads, 4) void gcm_kt_kernel(const GcmTableKey
                                                             tg_batch b,
                                                             const uint32_t* __restrict__ order,
                                                             const uint32_t* __restrict__ jobpos,
-                                                            const uint32_t* __restrict__ njobs_p) {
+                                                            const uint32_t* __restrict__ njobs_p,
+                                                            const uint32_t* __restrict__ nlong_p) {
     const uint32_t njobs = *njobs_p;
     if (blockIdx.x * kKtWaves >= njobs) return;   // the whole workgroup (uniform)
     stage_sbox(kKtSbox);
@@ -581,9 +563,12 @@ __global__ __launch_bounds__(kKtThreads, 4) void gcm_kt_kernel(const GcmTableKey
     const uint32_t wave = (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
     const uint32_t job = blockIdx.x * kKtWaves + wave;
     if (job >= njobs) return;
-    const uint32_t tab = 8192u * wave, recw = kKtRecBase + wave * 1024u;
     const uint32_t p0 = gld(jobpos, job), p1 = gld(jobpos, job + 1);
+    // the plan's tail (slots >= *nlong) holds the records this kernel leaves
+    // to the lane kernel: short ones and out-of-range key indices
+    if (p0 >= *nlong_p) return;
     const uint32_t k = (uint32_t)__builtin_amdgcn_readfirstlane((int)gld(b.key_idx, gld(order, p0)));
+    const uint32_t tab = 8192u * wave, recw = kKtRecBase + wave * 1024u;
     build_table4(tab, hpow[64u * k + 7u]);   // this wave's GHASH tables for the job's key
     __builtin_amdgcn_wave_barrier();
     b.n = p1;   // the job's slots are p0 .. p1 - 1 (at most eight)
@@ -600,21 +585,21 @@ __global__ void kt_planes_kernel(const GcmTableKey* __restrict__ keys, uint64_t 
     planes[t] = e < 32 * (nr + 1) ? bs8_mask_word(keys[k].rk, e) : 0u;
 }
 
+// Key-table AES-GCM by record length (BASELINE config 4): records of at
+// least ``split`` bytes run the key-grouped octet kernel, the rest (and
+// records whose key_idx is not below nkeys) the lane-per-record kernel
+// (aes_gcm.hip gcm_table_vkernel) over the tail of the same plan, which the
+// planner leaves sorted by length, longest first.  split 0: every in-range
+// record takes the octet kernel; split ~0u: every record the lane kernel.
 template <int NR, bool OPEN>
 int launch_kt(const GcmTableKey* keys, uint64_t nkeys, const uint4* hpow, const uint32_t* planes,
-              const tg_batch& b, hipStream_t s) {
-    static bool attr_set = false;
-    if (!attr_set) {
-        if (hipFuncSetAttribute((const void*)gcm_kt_kernel<NR, OPEN>,
-                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)kKtLds) != hipSuccess)
-            return TG_EHIP;
-        attr_set = true;
-    }
+              const tg_batch& b, hipStream_t s, uint32_t split) {
+    if (lds_attr((const void*)gcm_kt_kernel<NR, OPEN>, (int)kKtLds)) return TG_EHIP;
     if (b.n == 0) return TG_OK;
     if (b.n > 0xfffffffeull || !b.key_idx) return TG_EINVAL;
     size_t plan = 0;
-    int rc = tg_key_job_plan(b.key_idx, b.len, b.fixed_len, b.n, nullptr, nullptr, nullptr, nullptr,
-                             &plan, s);
+    int rc = tg_key_job_plan(b.key_idx, b.len, b.fixed_len, b.n, nkeys, split, nullptr, nullptr, nullptr,
+                             nullptr, nullptr, &plan, s);
     if (rc) return rc;
     const size_t so = (b.n * 4 + 255) & ~(size_t)255, sj = ((b.n + 1) * 4 + 255) & ~(size_t)255;
     uint8_t* buf = nullptr;
@@ -622,16 +607,20 @@ int launch_kt(const GcmTableKey* keys, uint64_t nkeys, const uint4* hpow, const 
     uint32_t* order = reinterpret_cast<uint32_t*>(buf);
     uint32_t* jobpos = reinterpret_cast<uint32_t*>(buf + so);
     uint32_t* njobs = reinterpret_cast<uint32_t*>(buf + so + sj);
-    rc = tg_key_job_plan(b.key_idx, b.len, b.fixed_len, b.n, order, jobpos, njobs, buf + so + sj + 256,
-                         &plan, s);
-    if (!rc) {
-        const uint64_t maxjobs = (b.n + 7) / 8 + (nkeys < b.n ? nkeys : b.n);
+    uint32_t* nlong = njobs + 1;
+    rc = tg_key_job_plan(b.key_idx, b.len, b.fixed_len, b.n, nkeys, split, order, jobpos, njobs, nlong,
+                         buf + so + sj + 256, &plan, s);
+    if (!rc && split != 0xffffffffu) {
+        // jobs: at most ceil(c_k / 8) per distinct key k of the long records,
+        // i.e. n / 8 + min(n, nkeys), plus the tail's jobs (which exit at once)
+        const uint64_t maxjobs = (b.n + 7) / 8 + (nkeys < b.n ? nkeys : b.n) + 1;
         const uint64_t groups = (maxjobs + kKtWaves - 1) / kKtWaves;
         hipLaunchKernelGGL((gcm_kt_kernel<NR, OPEN>), dim3((unsigned)groups), dim3(kKtThreads), kKtLds, s,
                            keys, hpow, planes, b, (const uint32_t*)order, (const uint32_t*)jobpos,
-                           (const uint32_t*)njobs);
+                           (const uint32_t*)njobs, (const uint32_t*)nlong);
         rc = hipGetLastError() == hipSuccess ? TG_OK : TG_EHIP;
     }
+    if (!rc) rc = tg_launch_gcm_table_lane(keys, nkeys, NR, b, OPEN, s, order, nlong);
     if (hipFreeAsync(buf, s) != hipSuccess) return TG_EHIP;
     return rc;
 }
@@ -658,13 +647,13 @@ int tg_launch_gcm_bs8(const tg::GcmKeyDev* key, int rounds, const tg_batch& b, b
 }
 
 int tg_launch_gcm_kt(const tg::GcmTableKey* keys, uint64_t nkeys, const uint4* hpow, const uint32_t* planes,
-                     int rounds, const tg_batch& b, bool open, hipStream_t s) {
+                     int rounds, const tg_batch& b, bool open, hipStream_t s, uint32_t split) {
     if (rounds == 10)
-        return open ? tg::launch_kt<10, true>(keys, nkeys, hpow, planes, b, s)
-                    : tg::launch_kt<10, false>(keys, nkeys, hpow, planes, b, s);
+        return open ? tg::launch_kt<10, true>(keys, nkeys, hpow, planes, b, s, split)
+                    : tg::launch_kt<10, false>(keys, nkeys, hpow, planes, b, s, split);
     if (rounds == 14)
-        return open ? tg::launch_kt<14, true>(keys, nkeys, hpow, planes, b, s)
-                    : tg::launch_kt<14, false>(keys, nkeys, hpow, planes, b, s);
+        return open ? tg::launch_kt<14, true>(keys, nkeys, hpow, planes, b, s, split)
+                    : tg::launch_kt<14, false>(keys, nkeys, hpow, planes, b, s, split);
     return TG_EINVAL;
 }
 

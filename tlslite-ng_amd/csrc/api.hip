@@ -11,11 +11,16 @@
 #include <cstddef>
 #include <cstdio>
 #include <cstring>
+#include <mutex>
+#include <set>
 #include <string>
+#include <utility>
+#include <vector>
 
 #include "aes_bs8.h"
 #include "common.h"
 #include "host.h"
+#include "options.h"
 #include "tlsgpu.h"
 
 namespace {
@@ -48,7 +53,6 @@ using tg::host::le32;
 static_assert(sizeof(tg::GcmKeyDev) == sizeof(tg::host::GcmKeyImage), "GcmKeyDev image size");
 TG_SAME_OFFSET(rounds);
 TG_SAME_OFFSET(ghash);
-TG_SAME_OFFSET(bsmask);
 TG_SAME_OFFSET(hpow);
 TG_SAME_OFFSET(ghash64);
 TG_SAME_OFFSET(ghash8);
@@ -57,6 +61,19 @@ TG_SAME_OFFSET(bs8mask);
 
 }  // namespace
 
+// Staging of one per-record call in flight: a mapped pinned buffer, its
+// device twin (option stage_copy) and a stream.  A key keeps a pool of them:
+// a call takes a free slot (or makes one) and gives it back, so calls on
+// copies of one AEAD object (copy.copy shares the handle, recordlayer.py:262,
+// :913) from several threads never share a buffer -- ctypes releases the GIL
+// around every call.
+struct Stage {
+    uint8_t* h = nullptr;
+    uint8_t* d = nullptr;
+    size_t cap = 0;
+    hipStream_t stream = nullptr;
+};
+
 struct tg_key {
     int alg;
     size_t keylen;
@@ -64,13 +81,11 @@ struct tg_key {
     int device;
     int rounds;
     int taglen;             // 16, or 8 for AES-CCM_8
-    hipStream_t stream;
     void* dev_key;          // GcmKeyDev / GcmTableKey[nkeys] (AES-GCM),
                             // AesKeyDev[nkeys] (AES-CCM), ChachaKeyDev[nkeys]
-    // staging for the per-record drop-in path
-    uint8_t* h_stage;
-    uint8_t* d_stage;
-    size_t stage_cap;
+    std::mutex stage_mu;    // guards the two lists
+    std::vector<Stage*> stages;        // every slot of this key
+    std::vector<Stage*> free_stages;   // the idle ones
 };
 
 namespace {
@@ -82,18 +97,56 @@ int select_device(const tg_key* k) {
     return TG_OK;
 }
 
-int ensure_stage(tg_key* k, size_t bytes) {
-    if (bytes <= k->stage_cap) return TG_OK;
-    size_t cap = k->stage_cap ? k->stage_cap : 65536;
+void free_stage(Stage* st) {
+    if (st->h) (void)hipHostFree(st->h);
+    if (st->d) (void)hipFree(st->d);
+    if (st->stream) (void)hipStreamDestroy(st->stream);
+    delete st;
+}
+
+// A free staging slot of this key (a new one if all are in use); NULL on error.
+Stage* take_stage(tg_key* k) {
+    {
+        std::lock_guard<std::mutex> g(k->stage_mu);
+        if (!k->free_stages.empty()) {
+            Stage* st = k->free_stages.back();
+            k->free_stages.pop_back();
+            return st;
+        }
+    }
+    Stage* st = new (std::nothrow) Stage();
+    if (!st) {
+        fail(TG_ENOMEM, "out of host memory");
+        return nullptr;
+    }
+    hipError_t e = hipStreamCreateWithFlags(&st->stream, hipStreamNonBlocking);
+    if (e != hipSuccess) {
+        delete st;
+        fail(TG_EHIP, "hipStreamCreate: %s", hipGetErrorString(e));
+        return nullptr;
+    }
+    std::lock_guard<std::mutex> g(k->stage_mu);
+    k->stages.push_back(st);
+    return st;
+}
+
+void give_stage(tg_key* k, Stage* st) {
+    std::lock_guard<std::mutex> g(k->stage_mu);
+    k->free_stages.push_back(st);
+}
+
+int ensure_stage(Stage* st, size_t bytes) {
+    if (bytes <= st->cap) return TG_OK;
+    size_t cap = st->cap ? st->cap : 65536;
     while (cap < bytes) cap *= 2;
-    if (k->h_stage) (void)hipHostFree(k->h_stage);
-    if (k->d_stage) (void)hipFree(k->d_stage);
-    k->h_stage = nullptr;
-    k->d_stage = nullptr;
-    k->stage_cap = 0;
-    HIP_TRY(hipHostMalloc((void**)&k->h_stage, cap, hipHostMallocMapped));
-    HIP_TRY(hipMalloc((void**)&k->d_stage, cap));
-    k->stage_cap = cap;
+    if (st->h) (void)hipHostFree(st->h);
+    if (st->d) (void)hipFree(st->d);
+    st->h = nullptr;
+    st->d = nullptr;
+    st->cap = 0;
+    HIP_TRY(hipHostMalloc((void**)&st->h, cap, hipHostMallocMapped));
+    HIP_TRY(hipMalloc((void**)&st->d, cap));
+    st->cap = cap;
     return TG_OK;
 }
 
@@ -113,15 +166,6 @@ uint32_t* table_planes(const tg_key* k) {
                                        kTableHpowBytes * k->nkeys);
 }
 
-// Key-table AES-GCM batches above the wave-per-record sizes run the
-// key-grouped octet kernel (aes_gcm_bs8.hip gcm_kt_kernel, its own planner)
-// when TLSGPU_GCM_TABLE_VARIANT is 14, the lane kernel otherwise; 14 also
-// forces it for small batches (tests).
-int kt_choice() {
-    const char* e = getenv("TLSGPU_GCM_TABLE_VARIANT");
-    return e ? atoi(e) : -1;
-}
-
 // The table's derived arrays on the device: H^1..H^64 and the key planes.
 int table_derive(tg_key* k, hipStream_t s) {
     const auto* keys = static_cast<const tg::GcmTableKey*>(k->dev_key);
@@ -137,25 +181,54 @@ size_t dev_key_bytes(const tg_key* k) {
                         : sizeof(tg::GcmKeyDev);
 }
 
-// Batches that run a lane-per-record kernel (many keys, or more records than
-// the wave-per-record kernels take) with per-record lengths run longest
-// first (planner.hip): a wave then holds records of nearly one length instead
-// of idling behind its longest.
+// Batches that run a lane-per-record kernel (more records than the
+// wave-per-record kernels take) with per-record lengths run longest first
+// (planner.hip): a wave then holds records of nearly one length instead of
+// idling behind its longest.
 constexpr uint64_t kPlanMinRecords = 2049;
+
+// Key-table AES-GCM: records of at least this many bytes take the
+// key-grouped octet kernel, shorter ones the lane kernel (option kt_split).
+constexpr uint32_t kKtSplitDefault = 2048;
+
+int launch_kernels(tg_key* k, const tg_batch& b, bool open, hipStream_t s, const uint32_t* order) {
+    if (k->alg == TG_AES_GCM)
+        return tg_launch_gcm(static_cast<const tg::GcmKeyDev*>(k->dev_key), k->rounds, b, open, s, order);
+    return tg_launch_chacha(static_cast<const tg::ChachaKeyDev*>(k->dev_key), k->nkeys, b, open, s, order);
+}
+
+// Key-table AES-GCM (option gcm_table_variant): 0 = auto (length split:
+// octet kernel for the long records, lane kernel for the rest, one plan);
+// 1 = the lane kernel for every record; 5 = the wave-per-record kernel;
+// 14 = the octet kernel for every record.
+int launch_gcm_table(tg_key* k, const tg_batch& b, bool open, hipStream_t s) {
+    const auto* keys = static_cast<const tg::GcmTableKey*>(k->dev_key);
+    uint32_t split;
+    switch (tg::opt(tg::kOptGcmTableVariant)) {
+        case 0: {
+            const int o = tg::opt(tg::kOptKtSplit);
+            split = o > 0 ? (uint32_t)o : kKtSplitDefault;
+            break;
+        }
+        case 1: split = 0xffffffffu; break;
+        case 5: return tg_launch_gcm_table_wave(keys, k->nkeys, table_hpow(k), k->rounds, b, open, s);
+        case 14: split = 0; break;
+        default: return TG_EINVAL;
+    }
+    return tg_launch_gcm_kt(keys, k->nkeys, table_hpow(k), table_planes(k), k->rounds, b, open, s, split);
+}
 
 // The order and the sort's scratch are allocated stream-ordered on the
 // launch's stream (hipMallocAsync / hipFreeAsync), so batches in flight on
 // other streams never share them.
-int launch_kernels(tg_key* k, const tg_batch& b, bool open, hipStream_t s, const uint32_t* order);
-
 int launch(tg_key* k, const tg_batch& b, bool open, hipStream_t s) {
-    const char* e = getenv("TLSGPU_NO_PLAN");
-    const bool wave = k->nkeys == 1 ? ((k->alg == TG_AES_GCM && tg_gcm_wave_path(b.n)) ||
-                                       (k->alg == TG_CHACHA20_POLY1305 && tg_chacha_wave_path(b.n)))
-                                    : k->alg == TG_AES_GCM && tg_gcm_table_wave_path(b.n);
-    const bool kt = k->alg == TG_AES_GCM && k->nkeys > 1 && kt_choice() == 14;   // plans its own jobs
-    if (!b.len || b.n < kPlanMinRecords || wave || kt || is_ccm(k->alg) || b.n > 0xffffffffull ||
-        (e && atoi(e)))
+    if (is_ccm(k->alg))
+        return tg_launch_ccm(static_cast<const tg::AesKeyDev*>(k->dev_key), k->nkeys, k->rounds, k->taglen,
+                             b, open, s);
+    if (k->alg == TG_AES_GCM && k->nkeys > 1) return launch_gcm_table(k, b, open, s);
+    const bool wave = k->nkeys == 1 && ((k->alg == TG_AES_GCM && tg_gcm_wave_path(b.n)) ||
+                                        (k->alg == TG_CHACHA20_POLY1305 && tg_chacha_wave_path(b.n)));
+    if (!b.len || b.n < kPlanMinRecords || wave || b.n > 0xffffffffull || tg::opt(tg::kOptNoPlan))
         return launch_kernels(k, b, open, s, nullptr);
     size_t scratch = 0;
     int rc = tg_length_order(b.len, b.n, nullptr, nullptr, &scratch, s);
@@ -170,23 +243,53 @@ int launch(tg_key* k, const tg_batch& b, bool open, hipStream_t s) {
     return rc;
 }
 
-int launch_kernels(tg_key* k, const tg_batch& b, bool open, hipStream_t s, const uint32_t* order) {
-    if (is_ccm(k->alg))
-        return tg_launch_ccm(static_cast<const tg::AesKeyDev*>(k->dev_key), k->nkeys > 1,
-                             k->rounds, k->taglen, b, open, s);
-    if (k->alg == TG_AES_GCM && k->nkeys > 1 && !order && kt_choice() == 14)
-        return tg_launch_gcm_kt(static_cast<const tg::GcmTableKey*>(k->dev_key), k->nkeys, table_hpow(k),
-                                table_planes(k), k->rounds, b, open, s);
-    if (k->alg == TG_AES_GCM && k->nkeys > 1)
-        return tg_launch_gcm_table(static_cast<const tg::GcmTableKey*>(k->dev_key), table_hpow(k),
-                                   k->rounds, b, open, s, order);
-    if (k->alg == TG_AES_GCM)
-        return tg_launch_gcm(static_cast<const tg::GcmKeyDev*>(k->dev_key), k->rounds, b, open, s,
-                             order);
-    return tg_launch_chacha(static_cast<const tg::ChachaKeyDev*>(k->dev_key), b, open, s, order);
-}
-
 size_t align16(size_t v) { return (v + 15) & ~(size_t)15; }
+
+// The record's round trip through one staging slot (single()).
+int single_staged(tg_key* k, Stage* st, const uint8_t* nonce, const uint8_t* aad, size_t aadlen,
+                  const uint8_t* in, size_t inlen, uint8_t* out, bool open, size_t len, size_t outlen,
+                  size_t o_aad, size_t o_in, size_t o_out, size_t o_st, size_t total) {
+    int rc = ensure_stage(st, total);
+    if (rc) return rc;
+    memcpy(st->h, nonce, 12);
+    if (aadlen) memcpy(st->h + o_aad, aad, aadlen);
+    if (inlen) memcpy(st->h + o_in, in, inlen);
+    // Zero copy by default: the kernel reads and writes the mapped pinned
+    // staging buffer over PCIe, so a record costs one launch and one
+    // synchronisation instead of two copies more (option stage_copy: copy
+    // through device memory instead).
+    const bool copy = tg::opt(tg::kOptStageCopy) != 0;
+    uint8_t* base = st->d;
+    if (!copy) {
+        void* dp = nullptr;
+        HIP_TRY(hipHostGetDevicePointer(&dp, st->h, 0));
+        base = static_cast<uint8_t*>(dp);
+    } else {
+        HIP_TRY(hipMemcpyAsync(st->d, st->h, o_out, hipMemcpyHostToDevice, st->stream));
+    }
+    tg_batch b;
+    memset(&b, 0, sizeof(b));
+    b.n = 1;
+    b.in = base + o_in;
+    b.fixed_len = (uint32_t)len;
+    b.fixed_aad_len = (uint32_t)aadlen;
+    b.out = base + o_out;
+    b.nonce = base;
+    b.aad = base + o_aad;
+    b.status = open ? base + o_st : nullptr;
+    if ((rc = launch(k, b, open, st->stream))) return fail(rc, "kernel launch failed");
+    if (copy)
+        HIP_TRY(hipMemcpyAsync(st->h + o_out, st->d + o_out, total - o_out, hipMemcpyDeviceToHost, st->stream));
+    HIP_TRY(hipStreamSynchronize(st->stream));
+    if (open) {
+        const int ok = st->h[o_st] == 1;
+        if (ok && len) memcpy(out, st->h + o_out, len);
+        if (!ok && len) memset(out, 0, len);
+        return ok;
+    }
+    memcpy(out, st->h + o_out, outlen);
+    return TG_OK;
+}
 
 // One record through the staging buffers: [nonce | aad | input | output | status]
 int single(tg_key* k, const uint8_t* nonce, size_t noncelen, const uint8_t* aad, size_t aadlen,
@@ -207,47 +310,12 @@ int single(tg_key* k, const uint8_t* nonce, size_t noncelen, const uint8_t* aad,
     const size_t o_st = align16(o_out + outlen), total = o_st + 16;
     int rc = select_device(k);
     if (rc) return rc;
-    if ((rc = ensure_stage(k, total))) return rc;
-    memcpy(k->h_stage, nonce, 12);
-    if (aadlen) memcpy(k->h_stage + o_aad, aad, aadlen);
-    if (inlen) memcpy(k->h_stage + o_in, in, inlen);
-    // Zero copy by default: the kernel reads and writes the mapped pinned
-    // staging buffer over PCIe, so a record costs one launch and one
-    // synchronisation instead of two copies more (TLSGPU_STAGE_COPY=1: copy
-    // through device memory instead).
-    const char* ce = getenv("TLSGPU_STAGE_COPY");
-    const bool copy = ce && atoi(ce);
-    uint8_t* base = k->d_stage;
-    if (!copy) {
-        void* dp = nullptr;
-        HIP_TRY(hipHostGetDevicePointer(&dp, k->h_stage, 0));
-        base = static_cast<uint8_t*>(dp);
-    } else {
-        HIP_TRY(hipMemcpyAsync(k->d_stage, k->h_stage, o_out, hipMemcpyHostToDevice, k->stream));
-    }
-    tg_batch b;
-    memset(&b, 0, sizeof(b));
-    b.n = 1;
-    b.in = base + o_in;
-    b.fixed_len = (uint32_t)len;
-    b.fixed_aad_len = (uint32_t)aadlen;
-    b.out = base + o_out;
-    b.nonce = base;
-    b.aad = base + o_aad;
-    b.status = open ? base + o_st : nullptr;
-    if ((rc = launch(k, b, open, k->stream))) return fail(rc, "kernel launch failed");
-    if (copy)
-        HIP_TRY(hipMemcpyAsync(k->h_stage + o_out, k->d_stage + o_out, total - o_out,
-                               hipMemcpyDeviceToHost, k->stream));
-    HIP_TRY(hipStreamSynchronize(k->stream));
-    if (open) {
-        const int ok = k->h_stage[o_st] == 1;
-        if (ok && len) memcpy(out, k->h_stage + o_out, len);
-        if (!ok && len) memset(out, 0, len);
-        return ok;
-    }
-    memcpy(out, k->h_stage + o_out, outlen);
-    return TG_OK;
+    Stage* st = take_stage(k);
+    if (!st) return TG_ENOMEM;
+    rc = single_staged(k, st, nonce, aad, aadlen, in, inlen, out, open, len, outlen, o_aad, o_in, o_out,
+                       o_st, total);
+    give_stage(k, st);
+    return rc;
 }
 
 int batch(tg_key* k, const tg_batch* b, void* stream, bool open) {
@@ -366,11 +434,6 @@ int new_key(int alg, size_t keylen, size_t nkeys, tg_key** out) {
     k->taglen = alg == TG_AES_CCM_8 ? 8 : 16;
     k->rounds = alg == TG_CHACHA20_POLY1305 ? 0 : (keylen == 16 ? 10 : 14);
     k->device = dev;
-    hipError_t e = hipStreamCreateWithFlags(&k->stream, hipStreamNonBlocking);
-    if (e != hipSuccess) {
-        delete k;
-        return fail(TG_EHIP, "hipStreamCreate: %s", hipGetErrorString(e));
-    }
     *out = k;
     return TG_OK;
 }
@@ -412,6 +475,23 @@ int hkdf_message(int hashlen, const uint8_t* label, size_t labellen, const uint8
 
 }  // namespace
 
+namespace tg {
+
+int lds_attr(const void* fn, int bytes) {
+    static std::mutex mu;
+    static std::set<std::pair<const void*, int>> done;   // (kernel, device)
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return TG_EHIP;
+    std::lock_guard<std::mutex> g(mu);
+    if (done.count({fn, dev})) return TG_OK;
+    if (hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, bytes) != hipSuccess)
+        return TG_EHIP;
+    done.insert({fn, dev});
+    return TG_OK;
+}
+
+}  // namespace tg
+
 extern "C" {
 
 const char* tg_version(void) { return "tlsgpu 0.1.0 (gfx950)"; }
@@ -427,6 +507,20 @@ int tg_device_count(int* count) {
         return fail(TG_ENODEV, "hipGetDeviceCount: %s", hipGetErrorString(e));
     }
     *count = n;
+    return TG_OK;
+}
+
+int tg_set_option(const char* name, int value) {
+    const int o = tg::opt_index(name);
+    if (o < 0) return fail(TG_EINVAL, "unknown option %s", name ? name : "(null)");
+    tg::opt_set(static_cast<tg::Opt>(o), value);
+    return TG_OK;
+}
+
+int tg_get_option(const char* name, int* value) {
+    const int o = tg::opt_index(name);
+    if (o < 0 || !value) return fail(TG_EINVAL, "unknown option %s", name ? name : "(null)");
+    *value = tg::opt(static_cast<tg::Opt>(o));
     return TG_OK;
 }
 
@@ -573,9 +667,7 @@ int tg_key_destroy(tg_key* k) {
         (void)hipMemset(k->dev_key, 0, dev_key_bytes(k));
         (void)hipFree(k->dev_key);
     }
-    if (k->h_stage) (void)hipHostFree(k->h_stage);
-    if (k->d_stage) (void)hipFree(k->d_stage);
-    if (k->stream) (void)hipStreamDestroy(k->stream);
+    for (Stage* st : k->stages) free_stage(st);   // no call may be in flight on k any more
     if (cur >= 0 && cur != k->device) (void)hipSetDevice(cur);
     delete k;
     return TG_OK;

@@ -15,6 +15,7 @@
 #include <cstdlib>
 
 #include "common.h"
+#include "options.h"
 #include "poly1305.h"
 
 namespace tg {
@@ -124,14 +125,14 @@ __device__ __forceinline__ uint32_t swz(uint32_t r, uint32_t c) { return c ^ ((r
 // instructions, as with 64-byte rows.  The keystream/Poly1305 pipeline is
 // the same as full_blocks(); a lane's next keystream block is b + 1.
 template <bool OPEN>
-__device__ __forceinline__ void tiled_blocks(WaveTile& t, uint32_t lane, uint32_t nvalid,
+__device__ __forceinline__ void tiled_blocks(WaveTile& t, uint32_t lane,
                                              const uint32_t (&k)[8], uint4 nv, uint32_t jmin,
                                              Poly32& p, uint32_t (&ks)[16]) {
     const uint32_t grp = lane >> 5, cq = lane & 7u, rq = lane >> 3;
     // the coalesced ops of group g's pair starting at block p0 (even)
     auto load_pair = [&](uint32_t g, uint32_t p0, uint4 (&R)[4]) {
         // unconditional: a chunk past the tile's blocks re-reads block 0 of
-        // its record (rows past the batch hold the last record's pointers),
+        // its record (rows without a record of their own read a valid row's),
         // so no branch leaves a load into R pending on some paths only
         const uint32_t off = p0 + (cq >> 2) < jmin ? 64 * p0 + 16 * cq : 16 * (cq & 3u);
 #pragma unroll
@@ -157,7 +158,7 @@ __device__ __forceinline__ void tiled_blocks(WaveTile& t, uint32_t lane, uint32_
             const uint4 v = t.row[r][swz(r, cq)];
             const uint4 pr = t.ptr[r];
             uint8_t* dst = reinterpret_cast<uint8_t*>(((uint64_t)pr.w << 32) | pr.z);
-            if (r < nvalid && blk < jmin) gstore16(dst + 64 * p0 + 16 * cq, v);
+            if (blk < jmin && dst) gstore16(dst + 64 * p0 + 16 * cq, v);
         }
     };
     // The pair finished in iteration i is stored at the top of iteration
@@ -172,7 +173,7 @@ __device__ __forceinline__ void tiled_blocks(WaveTile& t, uint32_t lane, uint32_
             const uint32_t r = 32 * g + 8 * q + rq;
             const uint4 pr = t.ptr[r];
             uint8_t* dst = reinterpret_cast<uint8_t*>(((uint64_t)pr.w << 32) | pr.z);
-            if (r < nvalid && blk < jmin) gstore16(dst + 64 * p0 + 16 * cq, S[q]);
+            if (blk < jmin && dst) gstore16(dst + 64 * p0 + 16 * cq, S[q]);
         }
     };
     auto read_pair = [&](uint32_t g, uint4 (&S)[4]) {
@@ -186,7 +187,7 @@ __device__ __forceinline__ void tiled_blocks(WaveTile& t, uint32_t lane, uint32_
     load_pair(0, 0, R);
     for (uint32_t i = 0; i <= jmin; ++i) {
         // group A's pair (i, i + 1) at even i, group B's (i - 1, i) at odd i
-        const uint32_t g = i & 1u, p0 = i - g;
+        const uint32_t g = i & 1u;
         // the pair finished in iteration i - 1: group A's (i - 2, i - 1) at
         // even i >= 2, group B's (i - 3, i - 2) at odd i >= 3
         const bool fl = (i >= 2 && !(i & 1u)) || (i >= 3 && (i & 1u));
@@ -201,14 +202,18 @@ __device__ __forceinline__ void tiled_blocks(WaveTile& t, uint32_t lane, uint32_
         const bool act = i >= grp && b < jmin;
         uint4 m[4];
         if (act) {
+            // the row's four chunks are read together and written back
+            // together: one LDS round trip instead of four dependent ones
             const uint32_t h = 4 * (b & 1u);
+            uint4 d[4];
+#pragma unroll
+            for (int c = 0; c < 4; ++c) d[c] = t.row[lane][swz(lane, h + c)];
 #pragma unroll
             for (int c = 0; c < 4; ++c) {
-                const uint4 d = t.row[lane][swz(lane, h + c)];
-                const uint4 ct = make_uint4(d.x ^ ks[4 * c], d.y ^ ks[4 * c + 1], d.z ^ ks[4 * c + 2],
-                                            d.w ^ ks[4 * c + 3]);
+                const uint4 ct = make_uint4(d[c].x ^ ks[4 * c], d[c].y ^ ks[4 * c + 1], d[c].z ^ ks[4 * c + 2],
+                                            d[c].w ^ ks[4 * c + 3]);
                 t.row[lane][swz(lane, h + c)] = ct;
-                m[c] = OPEN ? d : ct;
+                m[c] = OPEN ? d[c] : ct;
             }
         }
         __builtin_amdgcn_wave_barrier();
@@ -228,9 +233,12 @@ __device__ __forceinline__ void tiled_blocks(WaveTile& t, uint32_t lane, uint32_
     if (jmin & 1u) store_pair(1, jmin - 1);
 }
 
+// A key-table record whose key_idx is not below nkeys is skipped (open:
+// status 0): its row still serves the wave's coalesced transfers, with its
+// output pointer cleared so the tile never stores it.
 template <bool OPEN, bool MULTIKEY, int MINW>
 __global__ __launch_bounds__(kChachaThreads, MINW) void chacha_kernel(
-    const ChachaKeyDev* __restrict__ keys, tg_batch b, const uint32_t* __restrict__ order) {
+    const ChachaKeyDev* __restrict__ keys, uint64_t nkeys, tg_batch b, const uint32_t* __restrict__ order) {
     __shared__ WaveTile tiles[kWavesPerGroup];
     const uint64_t i_raw = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const uint32_t lane = threadIdx.x & 63;
@@ -238,12 +246,19 @@ __global__ __launch_bounds__(kChachaThreads, MINW) void chacha_kernel(
     if (wave_base >= b.n) return;  // whole wave idle (uniform)
     // Lanes past the end of the batch stay alive to serve the wave's
     // coalesced transfers, but work on a clamped record and never store.
-    const bool valid = i_raw < b.n;
-    const uint64_t t = valid ? i_raw : b.n - 1;
+    const uint64_t t = i_raw < b.n ? i_raw : b.n - 1;
     const uint64_t i = order ? order[t] : t;   // planner.hip: records longest first
-    const uint32_t nvalid = b.n - wave_base < 64 ? (uint32_t)(b.n - wave_base) : 64u;
+    uint32_t ki = 0;
+    if (MULTIKEY) {
+        ki = b.key_idx[i];
+        if (ki >= nkeys) {
+            if (OPEN && b.status && i_raw < b.n) b.status[i] = 0;
+            ki = 0;
+        }
+    }
+    const bool valid = i_raw < b.n && (!MULTIKEY || b.key_idx[i] < nkeys);
     uint32_t k[8];
-    const ChachaKeyDev* kp = keys + (MULTIKEY ? b.key_idx[i] : 0);
+    const ChachaKeyDev* kp = keys + ki;
 #pragma unroll
     for (int w = 0; w < 8; ++w) k[w] = kp->k[w];
 
@@ -254,6 +269,8 @@ __global__ __launch_bounds__(kChachaThreads, MINW) void chacha_kernel(
     const uint32_t alen = rec_aad_len(b, i);
     const bool aligned = (((uintptr_t)in | (uintptr_t)out) & 15) == 0;
     const uint4 nv = load_partial(b.nonce + 12 * i, 12);
+    // the tile stores a row only with a non-null output pointer
+    uint8_t* const tile_out = valid ? out : nullptr;
 
     Poly32 p;   // radix 2^32 (poly1305.h)
     {
@@ -270,15 +287,22 @@ __global__ __launch_bounds__(kChachaThreads, MINW) void chacha_kernel(
     const uint32_t nfull = len >> 6;
     uint32_t ks[16];
     chacha_block(k, 1, nv.x, nv.y, nv.z, ks);
-    // Coalesced tile path for the blocks every record of the wave has.
-    const uint32_t jmin = __all(!valid || aligned) ? wave_min(valid ? nfull : 0xffffffffu) : 0;
+    // Coalesced tile path for the blocks every record of the wave has.  Rows
+    // of lanes without a record of their own (past the batch, or a skipped
+    // key) load from the first valid lane's record, which has >= jmin blocks.
+    const uint64_t vmask = __ballot(valid);
+    const uint32_t jmin = (vmask && __all(!valid || aligned)) ? wave_min(valid ? nfull : 0xffffffffu) : 0;
     uint32_t j0 = 0;
     if (jmin > 0) {
         WaveTile& t = tiles[threadIdx.x >> 6];
-        t.ptr[lane] = make_uint4((uint32_t)(uintptr_t)in, (uint32_t)((uintptr_t)in >> 32),
-                                 (uint32_t)(uintptr_t)out, (uint32_t)((uintptr_t)out >> 32));
+        const int src = __ffsll((unsigned long long)vmask) - 1;
+        const uint32_t in_lo = (uint32_t)__shfl((int)(uint32_t)(uintptr_t)in, src, 64);
+        const uint32_t in_hi = (uint32_t)__shfl((int)(uint32_t)((uintptr_t)in >> 32), src, 64);
+        const uint8_t* tile_in = valid ? in : reinterpret_cast<const uint8_t*>(((uint64_t)in_hi << 32) | in_lo);
+        t.ptr[lane] = make_uint4((uint32_t)(uintptr_t)tile_in, (uint32_t)((uintptr_t)tile_in >> 32),
+                                 (uint32_t)(uintptr_t)tile_out, (uint32_t)((uintptr_t)tile_out >> 32));
         __builtin_amdgcn_wave_barrier();
-        tiled_blocks<OPEN>(t, lane, nvalid, k, nv, jmin, p, ks);
+        tiled_blocks<OPEN>(t, lane, k, nv, jmin, p, ks);
         j0 = jmin;
     }
     if (valid) {
@@ -441,36 +465,32 @@ __global__ __launch_bounds__(chacha_wave_threads<W>()) void chacha_wave_kernel(
 // profiles/r01/v21_smallbatch.txt).
 constexpr uint64_t kWaveMaxRecords = 49152;
 
-template <bool OPEN, bool MULTIKEY, int MINW>
-int launch_w(const ChachaKeyDev* keys, const tg_batch& b, hipStream_t s, const uint32_t* order) {
+template <bool OPEN, bool MULTIKEY>
+int launch_w(const ChachaKeyDev* keys, uint64_t nkeys, const tg_batch& b, hipStream_t s, const uint32_t* order) {
     const uint64_t blocks = (b.n + kChachaThreads - 1) / kChachaThreads;
-    hipLaunchKernelGGL((chacha_kernel<OPEN, MULTIKEY, MINW>), dim3((unsigned)blocks),
-                       dim3(kChachaThreads), 0, s, keys, b, order);
+    if (blocks > 0x7fffffffull) return TG_EINVAL;
+    hipLaunchKernelGGL((chacha_kernel<OPEN, MULTIKEY, 4>), dim3((unsigned)blocks), dim3(kChachaThreads), 0, s,
+                       keys, nkeys, b, order);
     return hipGetLastError() == hipSuccess ? TG_OK : TG_EHIP;
 }
 
-// Variants (TLSGPU_CHACHA_VARIANT, read per launch; tests and measurement):
-// 0 = auto (wave per record up to kWaveMaxRecords records, else lane per
-// record at 4 waves per SIMD, i.e. <= 128 VGPRs), 1 / 2 = lane per record
-// asking for 5 / 6 waves per SIMD, 3 = wave per record, 4 = lane per record,
-// 5 = lane per record without an occupancy request.
-int chacha_variant() {
-    const char* e = getenv("TLSGPU_CHACHA_VARIANT");
-    return e ? atoi(e) : 0;
-}
-
+// Option chacha_variant (tests and measurement): 0 = auto (wave per record
+// up to kWaveMaxRecords records, else lane per record at 4 waves per SIMD,
+// i.e. <= 128 VGPRs; 5 and 6 waves per SIMD measured slower), 3 = wave per
+// record, 4 = lane per record.
 bool wave_path(uint64_t n) {
-    const int v = chacha_variant();
+    const int v = opt(kOptChachaVariant);
     return v == 3 || (v == 0 && n <= kWaveMaxRecords);
 }
 
 template <bool OPEN, bool MULTIKEY>
-int launch(const ChachaKeyDev* keys, const tg_batch& b, hipStream_t s, const uint32_t* order) {
-    const int v = chacha_variant();
+int launch(const ChachaKeyDev* keys, uint64_t nkeys, const tg_batch& b, hipStream_t s, const uint32_t* order) {
+    const int v = opt(kOptChachaVariant);
+    if (v != 0 && v != 3 && v != 4) return TG_EINVAL;
     if (!MULTIKEY && wave_path(b.n)) {
         // waves per record as in the GCM launcher (aes_gcm.hip waves_per_record)
-        const char* env = getenv("TLSGPU_WAVES_PER_RECORD");
-        const int w = env ? atoi(env) : b.n <= 512 ? 4 : 1;   // profiles/r01/v21_smallbatch.txt
+        const int o = opt(kOptWavesPerRecord);
+        const int w = o ? o : b.n <= 512 ? 4 : 1;   // profiles/r01/v21_smallbatch.txt
         const uint64_t groups = w == 1 ? (b.n + 3) / 4 : b.n;
         if (groups > 0x7fffffffull) return TG_EINVAL;
         if (w == 16)
@@ -479,17 +499,14 @@ int launch(const ChachaKeyDev* keys, const tg_batch& b, hipStream_t s, const uin
         else if (w == 4)
             hipLaunchKernelGGL((chacha_wave_kernel<OPEN, 4>), dim3((unsigned)groups), dim3(256), 0, s,
                                keys, b);
-        else
+        else if (w == 1)
             hipLaunchKernelGGL((chacha_wave_kernel<OPEN, 1>), dim3((unsigned)groups), dim3(256), 0, s,
                                keys, b);
+        else
+            return TG_EINVAL;
         return hipGetLastError() == hipSuccess ? TG_OK : TG_EHIP;
     }
-    switch (v) {
-        case 1: return launch_w<OPEN, MULTIKEY, 5>(keys, b, s, order);
-        case 2: return launch_w<OPEN, MULTIKEY, 6>(keys, b, s, order);
-        case 5: return launch_w<OPEN, MULTIKEY, 1>(keys, b, s, order);
-        default: return launch_w<OPEN, MULTIKEY, 4>(keys, b, s, order);
-    }
+    return launch_w<OPEN, MULTIKEY>(keys, nkeys, b, s, order);
 }
 
 // RecordLayer._getNonce (recordlayer.py:522-534) for a run of sequence numbers.
@@ -517,12 +534,14 @@ __global__ void nonce_kernel(int mode, uint4 iv, uint64_t seq0, uint64_t n, uint
 
 bool tg_chacha_wave_path(uint64_t n) { return tg::wave_path(n); }
 
-int tg_launch_chacha(const tg::ChachaKeyDev* keys, const tg_batch& b, bool open, hipStream_t s,
+int tg_launch_chacha(const tg::ChachaKeyDev* keys, uint64_t nkeys, const tg_batch& b, bool open, hipStream_t s,
                      const uint32_t* order) {
     const bool multi = b.key_idx != nullptr;
     if (open)
-        return multi ? tg::launch<true, true>(keys, b, s, order) : tg::launch<true, false>(keys, b, s, order);
-    return multi ? tg::launch<false, true>(keys, b, s, order) : tg::launch<false, false>(keys, b, s, order);
+        return multi ? tg::launch<true, true>(keys, nkeys, b, s, order)
+                     : tg::launch<true, false>(keys, nkeys, b, s, order);
+    return multi ? tg::launch<false, true>(keys, nkeys, b, s, order)
+                 : tg::launch<false, false>(keys, nkeys, b, s, order);
 }
 
 int tg_launch_nonces(int mode, const uint8_t* iv_host, uint64_t seq0, uint64_t n, uint8_t* out,

@@ -23,9 +23,6 @@ struct GcmKeyDev {
     uint32_t rounds;       // 10 (AES-128) or 14 (AES-256)
     uint32_t pad[3];
     uint4 ghash[kGhashEntries];
-    // bitsliced AES (aes_bs.h BsKeyMasks): plane mask (r, k, b) at (16 r + k) 8 + b
-    // = 0 or ~0 by bit b of byte k of rk_r ^ (r ? 0x63 : 0) (see bs_mask_word)
-    uint32_t bsmask[15 * 128];
     uint4 hpow[2048];      // H^1 .. H^kHPow, normal order (gcm_wave_kernel)
     uint4 ghash64[kGhashEntries];   // the 8-bit tables of H^64 (gcm_wave_kernel's stride)
     uint4 ghash8[kGhashEntries];    // the 8-bit tables of H^8 (gcm_bs8_kernel's stride)
@@ -225,6 +222,10 @@ struct RecScratch {
     uint8_t* dummy;       // 32 zero bytes: AEAD input of publicly-invalid records
 };
 
+// hipFuncSetAttribute(MaxDynamicSharedMemorySize) for ``fn`` on the current
+// device, once per (function, device); thread-safe (api.hip).  0 or TG_EHIP.
+int lds_attr(const void* fn, int bytes);
+
 // Compute units of the current device (grid size of the persistent kernels),
 // looked up once per device.
 inline int device_cus() {
@@ -254,32 +255,37 @@ int tg_launch_gcm_hy(const tg::GcmKeyDev* key, int rounds, const tg_batch& b, bo
                      hipStream_t s, const uint32_t* order);
 int tg_launch_gcm_bs8(const tg::GcmKeyDev* key, int rounds, const tg_batch& b, bool open,
                       hipStream_t s, const uint32_t* order);
-// hpow: the key table's GHASH powers (tg_launch_table_hpow), or NULL for the
-// lane-per-record kernels only.
-int tg_launch_gcm_table(const tg::GcmTableKey* keys, const uint4* hpow, int rounds,
-                        const tg_batch& b, bool open, hipStream_t s, const uint32_t* order = nullptr);
 // hpow[64 k + e - 1] = H_k^e (normal order), e = 1..64, for the n keys.
 int tg_launch_table_hpow(const tg::GcmTableKey* keys, uint64_t n, uint4* hpow, hipStream_t s);
-bool tg_gcm_table_wave_path(uint64_t n);
 int tg_length_order(const uint32_t* len, uint64_t n, uint32_t* order, void* scratch, size_t* bytes,
                     hipStream_t s);
-// Key-grouped octet jobs of a key-table batch (planner.hip).
+// Key-grouped octet jobs of a key-table batch (planner.hip): records of at
+// least ``split`` bytes with key_idx < nkeys in front, grouped by key; the
+// rest behind them from slot *nlong on, longest first.
 int tg_key_job_plan(const uint32_t* key_idx, const uint32_t* len, uint32_t fixed_len, uint64_t n,
-                    uint32_t* order, uint32_t* jobpos, uint32_t* njobs, void* scratch, size_t* bytes,
-                    hipStream_t s);
-// The key-table octet kernel (aes_gcm_bs8.hip): planes = per-key bitsliced
-// round-key planes (tg_launch_kt_planes), hpow = the keys' H^1..H^64.
+                    uint64_t nkeys, uint32_t split, uint32_t* order, uint32_t* jobpos, uint32_t* njobs,
+                    uint32_t* nlong, void* scratch, size_t* bytes, hipStream_t s);
+// Key-table AES-GCM (aes_gcm_bs8.hip launch_kt): records of at least
+// ``split`` bytes through the key-grouped octet kernel (planes = per-key
+// bitsliced round-key planes, tg_launch_kt_planes; hpow = the keys'
+// H^1..H^64), the others through the lane kernel.
 int tg_launch_gcm_kt(const tg::GcmTableKey* keys, uint64_t nkeys, const uint4* hpow, const uint32_t* planes,
-                     int rounds, const tg_batch& b, bool open, hipStream_t s);
+                     int rounds, const tg_batch& b, bool open, hipStream_t s, uint32_t split);
+// The key-table lane kernel over slots [*first, n) of ``order`` (first NULL:
+// all of them) and the key-table wave-per-record kernel (aes_gcm.hip).
+int tg_launch_gcm_table_lane(const tg::GcmTableKey* keys, uint64_t nkeys, int rounds, const tg_batch& b,
+                             bool open, hipStream_t s, const uint32_t* order, const uint32_t* first);
+int tg_launch_gcm_table_wave(const tg::GcmTableKey* keys, uint64_t nkeys, const uint4* hpow, int rounds,
+                             const tg_batch& b, bool open, hipStream_t s);
 int tg_launch_kt_planes(const tg::GcmTableKey* keys, uint64_t n, int rounds, uint32_t* planes,
                         hipStream_t s);
-int tg_launch_ccm(const tg::AesKeyDev* keys, bool table, int rounds, int taglen,
+int tg_launch_ccm(const tg::AesKeyDev* keys, uint64_t nkeys, int rounds, int taglen,
                   const tg_batch& b, bool open, hipStream_t s);
 // Whether a single-key batch of n records runs the wave-per-record kernel
 // (no length planning needed then).
 bool tg_gcm_wave_path(uint64_t n);
 bool tg_chacha_wave_path(uint64_t n);
-int tg_launch_chacha(const tg::ChachaKeyDev* keys, const tg_batch& b, bool open, hipStream_t s,
+int tg_launch_chacha(const tg::ChachaKeyDev* keys, uint64_t nkeys, const tg_batch& b, bool open, hipStream_t s,
                      const uint32_t* order = nullptr);
 int tg_launch_records_prep(const tg_records& r, bool seal, bool aes, int taglen,
                            const tg::RecScratch& s, hipStream_t st);

@@ -171,7 +171,6 @@ int gcm_key_image(const uint8_t* key, size_t keylen, GcmKeyImage* out) {
     uint8_t zero[16] = {0}, h[16];
     aes_encrypt(rkb, nr, zero, h);                      // H = E_K(0^128)
     ghash_tables(h, out->ghash);
-    for (int e = 0; e < 128 * (nr + 1); ++e) out->bsmask[e] = bs_mask_word(out->rk, e);
     uint32_t hn[4], p[4];                               // H^1 .. H^2048, normal order
     to_norm(h, hn);
     for (int w = 0; w < 4; ++w) p[w] = hn[w];

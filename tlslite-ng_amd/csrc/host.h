@@ -16,7 +16,6 @@ struct GcmKeyImage {
     uint32_t rounds;
     uint32_t pad[3];
     uint32_t ghash[16 * 256][4];
-    uint32_t bsmask[15 * 128];
     uint32_t hpow[2048][4];
     uint32_t ghash64[16 * 256][4];
     uint32_t ghash8[16 * 256][4];

@@ -65,15 +65,6 @@ TG_KM_HD void ghash_table_words(const uint32_t hv[4], int e, uint32_t w[4]) {
     }
 }
 
-// Entry e of GcmKeyDev::bsmask (aes_bs.h, lane-per-block bitslicing) from
-// the round-key words: plane mask (r, k, b) at (16 r + k) 8 + b = 0 or ~0 by
-// bit b of byte k of rk_r ^ (r ? 0x63 : 0).
-TG_KM_HD uint32_t bs_mask_word(const uint32_t* rk, int e) {
-    const int r = e >> 7, k = (e >> 3) & 15, bit = e & 7;
-    const uint32_t w = rk[4 * r + (k >> 2)] ^ (r ? 0x63636363u : 0u);
-    return ((w >> (8 * (k & 3) + bit)) & 1u) ? 0xffffffffu : 0u;
-}
-
 // Entry e = (4 r + i) * 8 + b of GcmKeyDev::bs8mask (aes_bs8.h, 8-block
 // bitslicing): byte c of the word is 0xff iff bit b of byte i of round-key
 // word rk[4 r + c] ^ (r ? 0x63636363 : 0) is set.

@@ -369,10 +369,10 @@ __global__ void hpow_kernel(GcmKeyDev* key) {
     key->hpow[e] = make_uint4(r[0], r[1], r[2], r[3]);
 }
 
-// GcmKeyDev::bsmask from the round keys (after aes_setup_kernel, layout 0).
+// GcmKeyDev::bs8mask from the round keys (after aes_setup_kernel, layout 0):
+// 32 (NR + 1) <= 480 planes.
 __global__ void bs_mask_kernel(GcmKeyDev* key) {
     const int e = blockIdx.x * blockDim.x + threadIdx.x;
-    if (e < 128 * (int)(key->rounds + 1)) key->bsmask[e] = bs_mask_word(key->rk, e);
     if (e < 32 * (int)(key->rounds + 1)) key->bs8mask[e] = bs8::mask_word(key->rk, e);
 }
 
@@ -422,7 +422,7 @@ int tg_launch_aes_setup(int keylen, int layout, const uint8_t* keys, uint64_t n,
         if (hipGetLastError() != hipSuccess) return TG_EHIP;
         hipLaunchKernelGGL(tg::ghash8_table_kernel, dim3(tg::kGhashEntries / 256), dim3(256), 0, s, k);
         if (hipGetLastError() != hipSuccess) return TG_EHIP;
-        hipLaunchKernelGGL(tg::bs_mask_kernel, dim3(15 * 128 / 256), dim3(256), 0, s, k);
+        hipLaunchKernelGGL(tg::bs_mask_kernel, dim3((15 * 32 + 255) / 256), dim3(256), 0, s, k);
         if (hipGetLastError() != hipSuccess) return TG_EHIP;
         if (hipMemsetAsync(&k->ghash[0], 0, sizeof(uint4), s) != hipSuccess) return TG_EHIP;
     }

@@ -1,0 +1,33 @@
+// options.h -- process-wide kernel-selection options of libtlsgpu.
+//
+// The launchers consult these instead of calling getenv on every launch.
+// Each option starts from its TLSGPU_* environment variable, read once per
+// process on first use, and tg_set_option (include/tlsgpu.h) changes it at
+// run time -- the tests force one kernel after another in a single process
+// that way.  0 always means "auto" (the engine's own choice).
+#pragma once
+
+namespace tg {
+
+enum Opt {
+    kOptGcmVariant = 0,       // TLSGPU_GCM_VARIANT: single-key AES-GCM kernel (aes_gcm.hip)
+    kOptGcmTableVariant,      // TLSGPU_GCM_TABLE_VARIANT: key-table AES-GCM kernel
+    kOptChachaVariant,        // TLSGPU_CHACHA_VARIANT
+    kOptCcmVariant,           // TLSGPU_CCM_VARIANT
+    kOptWavesPerRecord,       // TLSGPU_WAVES_PER_RECORD: 1 / 4 / 16, 0 = by batch size
+    kOptNoPlan,               // TLSGPU_NO_PLAN: 1 = no length-sorted launch order
+    kOptStageCopy,            // TLSGPU_STAGE_COPY: 1 = per-record calls copy through HBM
+    kOptHyT,                  // TLSGPU_HY_T: T-table waves of the hybrid kernel (0 = 8)
+    kOptHyNoPrio,             // TLSGPU_HY_NOPRIO: 1 = T-table waves at normal priority
+    kOptKtSplit,              // TLSGPU_KT_SPLIT: key-table length split in bytes, 0 = auto
+    kOptHyThreads,            // TLSGPU_HY_THREADS: hybrid AES-GCM workgroup, 0 = 1024, or 768
+    kOptCount
+};
+
+// The option's current value (environment value on first use, 0 if unset).
+int opt(Opt o);
+// Name -> option, or -1.
+int opt_index(const char* name);
+void opt_set(Opt o, int value);
+
+}  // namespace tg

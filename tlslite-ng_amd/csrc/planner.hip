@@ -44,12 +44,26 @@ int tg_length_order(const uint32_t* len, uint64_t n, uint32_t* order, void* scra
 // wave-uniform, one GHASH table per wave) and records of similar length.
 namespace {
 
+// Sort key: (key, length descending); records shorter than ``split`` or with
+// a key index not below nkeys get the tail key kTail (sorted last, by length).
+constexpr uint32_t kTail = 0xffffffffu;
+
 __global__ void kjp_keys(const uint32_t* __restrict__ key_idx, const uint32_t* __restrict__ len,
-                         uint32_t fixed_len, uint64_t n, uint64_t* __restrict__ ck) {
+                         uint32_t fixed_len, uint64_t n, uint64_t nkeys, uint32_t split,
+                         uint64_t* __restrict__ ck, uint32_t* __restrict__ nlong) {
     const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t == 0) *nlong = (uint32_t)n;   // no tail unless kjp_tail finds one
     if (t >= n) return;
     const uint32_t L = len ? len[t] : fixed_len;
-    ck[t] = ((uint64_t)key_idx[t] << 32) | (uint64_t)(0xffffffffu - L);
+    const uint32_t k = key_idx[t];
+    const uint32_t g = (k >= nkeys || L < split) ? kTail : k;
+    ck[t] = ((uint64_t)g << 32) | (uint64_t)(0xffffffffu - L);
+}
+
+__global__ void kjp_tail(const uint64_t* __restrict__ ck, uint64_t n, uint32_t* __restrict__ nlong) {
+    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= n) return;
+    if ((ck[t] >> 32) == kTail && (t == 0 || (ck[t - 1] >> 32) != kTail)) *nlong = (uint32_t)t;
 }
 
 __global__ void kjp_group_starts(const uint64_t* __restrict__ ck, uint64_t n, uint32_t* __restrict__ g) {
@@ -81,10 +95,12 @@ size_t ru256(size_t v) { return (v + 255) & ~(size_t)255; }
 
 // scratch == nullptr: *bytes = what a batch of n needs.  Outputs: order[n]
 // (record index per slot), jobpos[n + 1] (first slot of job j; jobpos[njobs]
-// = n), *njobs (device).  n < 2^32.
+// = n), *njobs and *nlong (device): slots [0, nlong) hold the records of at
+// least ``split`` bytes with key_idx < nkeys, grouped by key; slots
+// [nlong, n) the rest, longest first.  n < 2^32.
 int tg_key_job_plan(const uint32_t* key_idx, const uint32_t* len, uint32_t fixed_len, uint64_t n,
-                    uint32_t* order, uint32_t* jobpos, uint32_t* njobs, void* scratch, size_t* bytes,
-                    hipStream_t s) {
+                    uint64_t nkeys, uint32_t split, uint32_t* order, uint32_t* jobpos, uint32_t* njobs,
+                    uint32_t* nlong, void* scratch, size_t* bytes, hipStream_t s) {
     rocprim::counting_iterator<uint32_t> iota(0);
     size_t t_sort = 0, t_max = 0, t_sum = 0;
     if (rocprim::radix_sort_pairs(nullptr, t_sort, (uint64_t*)nullptr, (uint64_t*)nullptr, iota,
@@ -111,10 +127,12 @@ int tg_key_job_plan(const uint32_t* key_idx, const uint32_t* len, uint32_t fixed
     uint32_t* js = reinterpret_cast<uint32_t*>(p + 2 * b64 + 2 * b32);
     void* t = p + 2 * b64 + 3 * b32;
     const unsigned blocks = (unsigned)((n + 255) / 256);
-    hipLaunchKernelGGL(kjp_keys, dim3(blocks), dim3(256), 0, s, key_idx, len, fixed_len, n, ck);
+    hipLaunchKernelGGL(kjp_keys, dim3(blocks), dim3(256), 0, s, key_idx, len, fixed_len, n, nkeys, split,
+                       ck, nlong);
     size_t ts = t_sort;
     if (rocprim::radix_sort_pairs(t, ts, ck, ck_sorted, iota, order, (size_t)n, 0, 64, s) != hipSuccess)
         return TG_EHIP;
+    hipLaunchKernelGGL(kjp_tail, dim3(blocks), dim3(256), 0, s, ck_sorted, n, nlong);
     hipLaunchKernelGGL(kjp_group_starts, dim3(blocks), dim3(256), 0, s, ck_sorted, n, g);
     size_t tm = t_max;
     if (rocprim::inclusive_scan(t, tm, g, gs, (size_t)n, rocprim::maximum<uint32_t>(), s) != hipSuccess)

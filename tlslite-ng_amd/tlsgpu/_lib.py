@@ -31,7 +31,7 @@ EXPORTS = ("tg_version", "tg_last_error", "tg_device_count", "tg_init", "tg_key_
            "tg_open_batch", "tg_make_nonces", "tg_malloc", "tg_free", "tg_memcpy_h2d",
            "tg_memcpy_d2h", "tg_stream_sync", "tg_seal_records", "tg_open_records",
            "tg_hkdf_expand_label", "tg_key_create_device", "tg_scan_records", "tg_gather",
-           "tg_selftest_poly1305", "tg_selftest_ghash")
+           "tg_selftest_poly1305", "tg_selftest_ghash", "tg_set_option", "tg_get_option")
 
 TG_TLS12 = 0x0303
 TG_TLS13 = 0x0304
@@ -136,6 +136,8 @@ def load():
     l.tg_gather.argtypes = [p, p, p, p, p, u64, p]
     l.tg_selftest_poly1305.argtypes = [i, p, p, p, p, u64, p]
     l.tg_selftest_ghash.argtypes = [i, p, p, p, p, p, p, p, u64, p]
+    l.tg_set_option.argtypes = [ctypes.c_char_p, i]
+    l.tg_get_option.argtypes = [ctypes.c_char_p, ctypes.POINTER(ctypes.c_int)]
     for name in EXPORTS:
         if name not in ("tg_version", "tg_last_error"):
             getattr(l, name).restype = ctypes.c_int
@@ -150,6 +152,39 @@ def check(rc):
         msg = load().tg_last_error()
         raise TlsGpuError(rc, msg.decode() if msg else "")
     return rc
+
+
+def set_option(name, value):
+    """Set a process-wide kernel-selection option (include/tlsgpu.h
+    tg_set_option: gcm_variant, gcm_table_variant, kt_split, chacha_variant,
+    ccm_variant, waves_per_record, no_plan, stage_copy, hy_t, hy_noprio)."""
+    check(load().tg_set_option(name.encode(), int(value)))
+
+
+def get_option(name):
+    v = ctypes.c_int(0)
+    check(load().tg_get_option(name.encode(), ctypes.byref(v)))
+    return v.value
+
+
+class options(object):
+    """``with tlsgpu.options(gcm_variant=14): ...`` sets options for the block
+    and restores the previous values after it (tests force kernels this way)."""
+
+    def __init__(self, **kw):
+        self.kw = kw
+        self.old = {}
+
+    def __enter__(self):
+        for k, v in self.kw.items():
+            self.old[k] = get_option(k)
+            set_option(k, v)
+        return self
+
+    def __exit__(self, *exc):
+        for k, v in self.old.items():
+            set_option(k, v)
+        return False
 
 
 def device_count():

@@ -352,27 +352,40 @@ class RecordReader(object):
         self._pos = 0
         self._got = False
         self._dead = False
+        seq_entry = self.seq
         meta, done = [], []        # slots opened (metadata pending) / packed (copy pending)
         free = list(self.rslots)
         start = 0
         err = None
-        while not self._dead:
-            n, used, err = self._scan(start)
-            if n:
-                if not free:
-                    if not done:
+        try:
+            while not self._dead:
+                n, used, err = self._scan(start)
+                if n:
+                    if not free:
+                        if not done:
+                            done.append(self._pack(meta.pop(0), dst, direct, pieces))
+                        free.append(self._finish_read(done.pop(0), dst))
+                    s = free.pop(0)
+                    self._enqueue_open(s, start, n, used)
+                    start += used
+                    meta.append(s)
+                    if len(meta) > 1:
                         done.append(self._pack(meta.pop(0), dst, direct, pieces))
-                    free.append(self._finish_read(done.pop(0), dst))
-                s = free.pop(0)
-                self._enqueue_open(s, start, n, used)
-                start += used
-                meta.append(s)
-                if len(meta) > 1:
-                    done.append(self._pack(meta.pop(0), dst, direct, pieces))
-            if err is not None or n < self.batch:
-                break
-        while meta:
-            done.append(self._pack(meta.pop(0), dst, direct, pieces))
+                if err is not None or n < self.batch:
+                    break
+            while meta:
+                done.append(self._pack(meta.pop(0), dst, direct, pieces))
+        except _OutTooSmall:
+            # nothing of this call is delivered: wait for every slot still
+            # running (opens, and copies into ``out``), then undo the call --
+            # the sequence number and the wire bytes stay where they were, so
+            # a retry with a larger buffer returns the same bytes
+            for s in meta + done + self.rslots:
+                s.event.synchronize()
+            self.seq = seq_entry
+            self.pending_error = None
+            self._dead = False
+            raise ValueError("output buffer too small")
         while done:
             self._finish_read(done.pop(0), dst)
         # the unconsumed tail to the front (every copy from h_buf has finished)
@@ -454,7 +467,7 @@ class RecordReader(object):
         s.h_plen.numpy()[:k] = L.astype(np.int32)
         if dst is not None:
             if self._pos + total > len(dst):
-                raise ValueError("output buffer too small")
+                raise _OutTooSmall()
             s.target = (self._pos, total)
         else:
             piece = bytearray(total)
@@ -559,6 +572,10 @@ class RecordReader(object):
             self.h_out[:span].copy_(s.d_data[:span], non_blocking=True)
         s.stream.synchronize()
         return self.h_out.numpy()
+
+
+class _OutTooSmall(Exception):
+    """read_application_data: the caller's buffer cannot take a batch."""
 
 
 def read_application_data(reader):

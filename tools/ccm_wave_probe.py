@@ -1,5 +1,5 @@
 """AES-128-CCM latency of small batches and the per-record call: the wave-per-
-record kernel (TLSGPU_CCM_VARIANT=2) against the lane kernel (3), HIP-event
+record kernel (ccm_variant 2) against the lane kernel (3), HIP-event
 times on the launch stream, and createAESCCM(...).seal / open wall time for one
 16 KiB record (host buffers, the drop-in path).  usage: python tools/ccm_wave_probe.py"""
 import os
@@ -28,7 +28,7 @@ for n in (1, 8, 64, 512, 2048, 4096, 8192):
     line = []
     ref = None
     for variant in ("2", "3"):
-        os.environ["TLSGPU_CCM_VARIANT"] = variant
+        tlsgpu.set_option("ccm_variant", int(variant))
         for name, fn, b in (("seal", tlsgpu.seal_batch, sb), ("open", tlsgpu.open_batch, ob)):
             fn(o, b)
             torch.cuda.synchronize()
@@ -45,7 +45,7 @@ for n in (1, 8, 64, 512, 2048, 4096, 8192):
         else:
             assert torch.equal(ref, sealed)
     print("n=%5d x 16 KiB: %s" % (n, "  ".join(line)), flush=True)
-os.environ.pop("TLSGPU_CCM_VARIANT")
+tlsgpu.set_option("ccm_variant", 0)
 c = tlsgpu.createAESCCM(bytearray(range(16)))
 pt = bytearray(os.urandom(L))
 nonce = bytearray(12)

@@ -3,9 +3,10 @@ shape (2^20 x 16 KiB, TLS 1.3 AAD, 128-byte aligned sealed records), device
 resident, and check that every kernel's sealed bytes equal the first one's
 (the T-table kernel, itself pinned to the oracle by the -m gpu tests).
 
-    python tools/gcm_kernel_probe.py "0" "14" "15:TLSGPU_HY_T=8" ...
+    python tools/gcm_kernel_probe.py "0" "14" "15:hy_t=8" ...
 
-Each argument is VARIANT[:ENV=VALUE,...] (TLSGPU_GCM_VARIANT and extra env).
+Each argument is VARIANT[:OPTION=VALUE,...] (the gcm_variant option and extra
+tlsgpu options, include/tlsgpu.h tg_set_option).
 """
 import os
 import sys
@@ -40,15 +41,13 @@ def main():
                            out_stride=L, fixed_aad_len=5, status=status)
     ref = None
     for arg in sys.argv[1:]:
-        var, _, envs = arg.partition(":")
-        saved = {}
-        env = {"TLSGPU_GCM_VARIANT": var}
-        for kv in filter(None, envs.split(",")):
+        var, _, extra = arg.partition(":")
+        opts = {"gcm_variant": int(var)}
+        for kv in filter(None, extra.split(",")):
             k, v = kv.split("=")
-            env[k] = v
-        for k, v in env.items():
-            saved[k] = os.environ.get(k)
-            os.environ[k] = v
+            opts[k] = int(v)
+        ctx = tlsgpu.options(**opts)
+        ctx.__enter__()
         times = {}
         for name, batch, fn in (("seal", sb, tlsgpu.seal_batch), ("open", ob, tlsgpu.open_batch)):
             fn(key, batch)
@@ -74,11 +73,7 @@ def main():
         print("%-24s seal %7.3f ms (%6.1f GiB/s)  open %7.3f ms (%6.1f GiB/s)  roundtrip %s  same-as-first %s"
               % (arg, times["seal"], gib / times["seal"] * 1e3, times["open"],
                  gib / times["open"] * 1e3, ok_rt, same), flush=True)
-        for k, v in saved.items():
-            if v is None:
-                del os.environ[k]
-            else:
-                os.environ[k] = v
+        ctx.__exit__(None, None, None)
 
 
 if __name__ == "__main__":

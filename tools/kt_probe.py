@@ -1,5 +1,5 @@
 """Key-table AES-256-GCM seal time by record length: the lane-per-record
-kernel (TLSGPU_GCM_TABLE_VARIANT=0) against the key-grouped octet kernel (14)
+kernel (gcm_table_variant 1) against the key-grouped octet kernel (14)
 on 65 536 keys with uniformly random key_idx, fixed-length batches of
 64 B .. 16 KiB.  HIP-event times on the launch stream (torch's current).
 usage: python tools/kt_probe.py"""
@@ -26,8 +26,8 @@ for L, n in ((16384, 1 << 18), (4096, 1 << 20), (1024, 1 << 20), (256, 1 << 20),
     b = tlsgpu.make_batch(n, inp, out, nonces, aad=aad, lens=lens, in_stride=L, out_stride=L + 16,
                           fixed_aad_len=13, key_idx=kidx)
     row = []
-    for v in ("0", "14"):
-        os.environ["TLSGPU_GCM_TABLE_VARIANT"] = v
+    for v in ("1", "14"):
+        tlsgpu.set_option("gcm_table_variant", int(v))
         tlsgpu.seal_batch(table, b)
         torch.cuda.synchronize()
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)

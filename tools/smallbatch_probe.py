@@ -13,10 +13,8 @@ L, S = 16384, 16512
 REPS = 5
 
 
-def run(obj, n, env):
-    saved = {k: os.environ.get(k) for k in env}
-    os.environ.update(env)
-    try:
+def run(obj, n, opts):
+    with tlsgpu.options(**opts):
         inp = torch.randint(0, 256, (n * L,), dtype=torch.uint8, device="cuda")
         out = torch.empty(n * S, dtype=torch.uint8, device="cuda")
         nonces = torch.zeros(12 * n, dtype=torch.uint8, device="cuda")
@@ -35,37 +33,31 @@ def run(obj, n, env):
         torch.cuda.synchronize()
         us = e0.elapsed_time(e1) / REPS * 1e3
         return us, n * L / (us * 1e-6) / 2 ** 30
-    finally:
-        for k, v in saved.items():
-            if v is None:
-                del os.environ[k]
-            else:
-                os.environ[k] = v
 
 
 for name, obj, var, lane_v, wave_v in (
-        ("aes128gcm", tlsgpu.HipAESGCM(bytearray(16)), "TLSGPU_GCM_VARIANT", "7", "6"),
+        ("aes128gcm", tlsgpu.HipAESGCM(bytearray(16)), "gcm_variant", 16, 6),
         ("chacha20-poly1305", tlsgpu.HipCHACHA20_POLY1305(bytearray(32)),
-         "TLSGPU_CHACHA_VARIANT", "4", "3")):
+         "chacha_variant", 4, 3)):
     for n in (1, 4, 16, 64, 128, 256, 512, 1024, 2048, 4096, 16384, 65536):
         cols = []
         for label, env in (("lane", {var: lane_v}),
-                           ("wave1", {var: wave_v, "TLSGPU_WAVES_PER_RECORD": "1"}),
-                           ("wave4", {var: wave_v, "TLSGPU_WAVES_PER_RECORD": "4"}),
-                           ("wave16", {var: wave_v, "TLSGPU_WAVES_PER_RECORD": "16"})):
+                           ("wave1", {var: wave_v, "waves_per_record": 1}),
+                           ("wave4", {var: wave_v, "waves_per_record": 4}),
+                           ("wave16", {var: wave_v, "waves_per_record": 16})):
             us, g = run(obj, n, env)
             cols.append("%s %8.1f us %7.1f GiB/s" % (label, us, g))
         print("%-18s n=%5d  %s" % (name, n, "  ".join(cols)), flush=True)
 
 # where a record per lane overtakes a wave per record
 for name, obj, var, lane_v, wave_v in (
-        ("aes128gcm", tlsgpu.HipAESGCM(bytearray(16)), "TLSGPU_GCM_VARIANT", "7", "6"),
+        ("aes128gcm", tlsgpu.HipAESGCM(bytearray(16)), "gcm_variant", 16, 6),
         ("chacha20-poly1305", tlsgpu.HipCHACHA20_POLY1305(bytearray(32)),
-         "TLSGPU_CHACHA_VARIANT", "4", "3")):
+         "chacha_variant", 4, 3)):
     for n in (32768, 65536, 98304, 131072, 163840, 196608, 262144, 524288, 1048576):
         cols = []
         for label, env in (("lane", {var: lane_v}),
-                           ("wave1", {var: wave_v, "TLSGPU_WAVES_PER_RECORD": "1"})):
+                           ("wave1", {var: wave_v, "waves_per_record": 1})):
             us, g = run(obj, n, env)
             cols.append("%s %8.1f us %7.1f GiB/s" % (label, us, g))
         print("%-18s n=%7d  %s" % (name, n, "  ".join(cols)), flush=True)

@@ -10,9 +10,17 @@ under the same counter passes, and the factor of a shape is
 bytes / counter bytes; a kernel's traffic is its raw counters times the
 factors of its shape:
 
-  aes128gcm_*        gcm_hy_kernel (octet: 8 records x 128 B per instruction)
-  chacha20-poly1305_* chacha_kernel (octet too since round 2's line-pair tile;
-                      it was tile64, 16 records x 64 B per instruction)
+  aes128gcm_*         gcm_hy_kernel, octet layout: 8 records x 128 B per
+                      instruction -> the octet factors
+  chacha20-poly1305_* chacha_kernel, line-pair tile: the same 8 records x
+                      128 B per instruction -> the octet factors (round 1's
+                      tile moved 16 records x 64 B: tile64)
+  c4_kt_*             gcm_kt_kernel (config 4's long records), octet layout
+  c4_lane_*           gcm_table_vkernel (config 4's short records), 16 B per
+                      lane, one record per lane -> the lane factors
+
+Config 4 (bench.py --config c4) is one seal and one open of the whole batch;
+its traffic per operation is the sum over the kernels of that operation.
 
 The headline working set (48 GiB) is far past the 256 MiB Infinity Cache, so
 cache hits in the counters are negligible.
@@ -29,10 +37,15 @@ from collections import defaultdict
 
 CAL_BYTES = 16384 * (1 << 18)
 CAL = {"k_coalesced": "coalesced", "k_octet": "octet", "k_tile64": "tile64", "k_lane": "lane"}
-KERNELS = [(r"gcm_hy_kernel<10, false", "aes128gcm_seal", "octet"),
-           (r"gcm_hy_kernel<10, true", "aes128gcm_open", "octet"),
-           (r"chacha_kernel<false", "chacha20-poly1305_seal", "octet"),
-           (r"chacha_kernel<true", "chacha20-poly1305_open", "octet")]
+# (kernel name pattern, label, access shape, calibration shape)
+KERNELS = [(r"gcm_hy_kernel<10, false", "aes128gcm_seal", "octet", "octet"),
+           (r"gcm_hy_kernel<10, true", "aes128gcm_open", "octet", "octet"),
+           (r"chacha_kernel<false", "chacha20-poly1305_seal", "line-pair tile", "octet"),
+           (r"chacha_kernel<true", "chacha20-poly1305_open", "line-pair tile", "octet"),
+           (r"gcm_kt_kernel<14, false", "c4_kt_seal", "octet", "octet"),
+           (r"gcm_kt_kernel<14, true", "c4_kt_open", "octet", "octet"),
+           (r"gcm_table_vkernel<14, false", "c4_lane_seal", "lane", "lane"),
+           (r"gcm_table_vkernel<14, true", "c4_lane_open", "lane", "lane")]
 
 
 def collect(d, pattern):
@@ -60,11 +73,12 @@ def main(d):
     raw = collect(d, "bench_*")
     out = {}
     for name, c in raw.items():
-        for pat, lab, shape in KERNELS:
-            if re.search(pat, name) and shape in factors:
+        for pat, lab, shape, cal in KERNELS:
+            if re.search(pat, name) and cal in factors:
                 fetch, write = mean_kb(c["FETCH_SIZE"]), mean_kb(c["WRITE_SIZE"])
-                ff, wf = factors[shape]["fetch_factor"], factors[shape]["write_factor"]
+                ff, wf = factors[cal]["fetch_factor"], factors[cal]["write_factor"]
                 out[lab] = {"fetch_size_bytes": fetch, "write_size_bytes": write, "shape": shape,
+                            "calibrated_as": cal,
                             "fetch_factor": ff, "write_factor": wf,
                             "hbm_read_bytes": fetch * ff, "hbm_write_bytes": write * wf,
                             "hbm_bytes": fetch * ff + write * wf,
