@@ -64,15 +64,20 @@ int tg_init(int device);                   /* hipSetDevice for the calling threa
  *   gcm_variant        0 auto, 6 wave per record, 14 bitsliced octet,
  *                      15 hybrid octet, 16 T-table lane per record
  *   gcm_table_variant  0 auto (length split), 1 lane, 5 wave per record,
+ *                      6 wave per record with 4-bit GHASH tables,
  *                      14 key-grouped octet
  *   kt_split           key-table length split in bytes (0 = 2048)
+ *   kt_lpr             key-table long records: lanes per record of the
+ *                      key-grouped bitsliced kernel (8 / 16 / 32 / 64; 0 =
+ *                      32), -1 = the wave-per-record T-table kernel
  *   chacha_variant     0 auto, 3 wave per record, 4 lane per record
  *   ccm_variant        0 auto, 1 lane full rounds, 2 wave, 3 lane
  *   waves_per_record   0 auto, 1 / 4 / 16
  *   no_plan            1 = no length-sorted launch order
  *   stage_copy         1 = per-record calls copy through device memory
- *   hy_t, hy_noprio    hybrid AES-GCM kernel: T-table waves (0 = 8 of 16),
- *                      1 = T-table waves at normal priority
+ *   hy_t, hy_noprio    hybrid AES-GCM kernel: T-table waves (0 = half,
+ *                      -1 = none), 1 = T-table waves at normal priority
+ *   hy_threads         hybrid AES-GCM workgroup: 0 = 1024, or 768
  * An unknown name is TG_EINVAL; a variant a launcher does not know makes
  * its launches fail with TG_EINVAL. */
 int tg_set_option(const char* name, int value);

@@ -59,7 +59,11 @@ struct FoldedRows {
     }
 };
 
-template <int NR, bool FOLD>
+// SB: log2 of the lanes per record (3 = the octet kernels; 4..6 = the
+// key-grouped kernel with 16 / 32 / 64 lanes per record): block j of a
+// lane's batch beta has counter c0 + (j << SB) + (beta << (SB + 3)), c0 =
+// 2 + rho, rho < 2^SB.
+template <int NR, bool FOLD, int SB = 3>
 static int run(int klen, unsigned seed) {
     srand(seed);
     uint8_t key[32], rk[16 * 15], nonce[12];
@@ -79,22 +83,24 @@ static int run(int klen, unsigned seed) {
     int bad = 0, checked = 0;
     const uint32_t betas[] = {0, 1, 2, 3, 7, 15, 16, 255, 256, 1022, 1023, 1024, 1025,
                               65535, 65536, 0x3ffffe, 0x3fffff};
-    for (uint32_t c0 = 2; c0 <= 9; ++c0) {
-        uint32_t lane[6], kmask;
-        tg::bs8::lane_consts(c0, lane, kmask);
+    constexpr uint32_t L = 1u << SB;
+    for (uint32_t c0 = 2; c0 <= L + 1; c0 += (SB > 3 ? 3 : 1)) {
+        uint32_t lane[SB + 3], kmask;
+        tg::bs8::lane_consts<SB>(c0, lane, kmask);
         for (uint32_t beta : betas) {
+            if ((uint64_t)beta << (SB + 3) >= (1ull << 31)) continue;   // counters stay 32-bit
             uint32_t s[4][8], w[4][8];
             for (int i = 0; i < 4; ++i)
                 for (int b = 0; b < 8; ++b) s[i][b] = tg::bs8::rec_plane(u, 8 * i + b);
-            for (int b = 0; b < 6; ++b) s[3][b] ^= lane[b];
-            tg::bs8::ctr_planes<6, 16>(s, kmask, beta);
-            if ((beta + 1u) >> 10) tg::bs8::ctr_planes<16, 32>(s, kmask, beta);
+            for (int b = 0; b < SB + 3; ++b) s[3 - (b >> 3)][b & 7] ^= lane[b];
+            tg::bs8::ctr_planes<SB + 3, 16, SB + 3>(s, kmask, beta);
+            if ((beta + 1u) >> (16 - (SB + 3))) tg::bs8::ctr_planes<16, 32, SB + 3>(s, kmask, beta);
             if (FOLD)
                 tg::bs8::encrypt<NR>(s, kf, w);
             else
                 tg::bs8::encrypt<NR>(s, km, w);
             for (int j = 0; j < 8; ++j) {
-                const uint32_t ctr = c0 + 64u * beta + 8u * j;
+                const uint32_t ctr = c0 + (beta << (SB + 3)) + ((uint32_t)j << SB);
                 uint8_t blk[16], want[16];
                 memcpy(blk, nonce, 12);
                 blk[12] = (uint8_t)(ctr >> 24); blk[13] = (uint8_t)(ctr >> 16);
@@ -104,8 +110,8 @@ static int run(int klen, unsigned seed) {
                     const uint32_t got = w[q][j] ^ rkw[4 * NR + q] ^ 0x63636363u;
                     if (got != le(want + 4 * q)) {
                         if (bad < 5)
-                            fprintf(stderr, "NR=%d c0=%u beta=%u j=%d q=%d got %08x want %08x\n",
-                                    NR, c0, beta, j, q, got, le(want + 4 * q));
+                            fprintf(stderr, "NR=%d SB=%d c0=%u beta=%u j=%d q=%d got %08x want %08x\n",
+                                    NR, SB, c0, beta, j, q, got, le(want + 4 * q));
                         ++bad;
                     }
                 }
@@ -113,7 +119,7 @@ static int run(int klen, unsigned seed) {
             }
         }
     }
-    printf("NR=%d fold=%d seed=%u blocks=%d bad=%d\n", NR, (int)FOLD, seed, checked, bad);
+    printf("NR=%d fold=%d lanes=%u seed=%u blocks=%d bad=%d\n", NR, (int)FOLD, L, seed, checked, bad);
     return bad;
 }
 
@@ -125,6 +131,13 @@ int main() {
         bad += run<14, false>(32, 100 + seed);
         bad += run<10, true>(16, seed);
         bad += run<14, true>(32, 100 + seed);
+    }
+    // the key-grouped kernel's 16 / 32 / 64 lanes per record (key planes unfolded)
+    for (unsigned seed = 1; seed <= 2; ++seed) {
+        bad += run<14, false, 4>(32, 200 + seed);
+        bad += run<14, false, 5>(32, 300 + seed);
+        bad += run<14, false, 6>(32, 400 + seed);
+        bad += run<10, false, 5>(16, 500 + seed);
     }
     // the per-record plane of a lane equals the plain bit test (GcmKeyDev::bs8mask layout)
     printf(bad ? "FAIL\n" : "OK\n");

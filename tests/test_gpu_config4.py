@@ -10,15 +10,15 @@ import pytest
 pytestmark = pytest.mark.gpu
 
 
-# auto (length split: octet kernel for the long records, lane kernel for the
-# rest) / lane kernel for all / key-grouped octet kernel for all
-@pytest.mark.parametrize("variant", [0, 1, 14])
-def test_config4_full_shape_sampled(oracle_mod, variant):
+# auto (length split: octet or wave-per-record kernel for the long records,
+# lane kernel for the rest) / lane kernel for all / octet kernel for all
+@pytest.mark.parametrize("variant,lpr", [(0, 0), (0, 32), (0, 64), (1, 0), (14, 0)])
+def test_config4_full_shape_sampled(oracle_mod, variant, lpr):
     import torch
     import tlsgpu
     if not torch.cuda.is_available():
         pytest.fail("GPU tests need a visible MI355X")
-    with tlsgpu.options(gcm_table_variant=variant):
+    with tlsgpu.options(gcm_table_variant=variant, kt_lpr=lpr):
         _run_config4(torch, tlsgpu, oracle_mod)
 
 

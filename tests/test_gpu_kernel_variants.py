@@ -25,28 +25,30 @@ def tg(torch):
 LENS = [0, 1, 15, 16, 17, 63, 64, 65, 1000, 1024, 1040, 4095, 16383, 16384, 16385, 16400]
 
 
-@pytest.mark.parametrize("alg,klen,opt,value", [
-    ("aesgcm", 16, "gcm_variant", 16),          # T-table lane per record
-    ("aesgcm", 32, "gcm_variant", 16),
-    ("aesgcm", 16, "gcm_variant", 6),           # wave per record
-    ("aesgcm", 32, "gcm_variant", 6),
-    ("aesgcm", 16, "gcm_variant", 14),          # 8-block bitsliced, octet per record
-    ("aesgcm", 32, "gcm_variant", 14),
-    ("aesgcm", 16, "gcm_variant", 15),          # hybrid T-table + bitsliced (persistent)
-    ("aesgcm", 32, "gcm_variant", 15),
-    ("chacha", 32, "chacha_variant", 4),        # lane per record
-    ("chacha", 32, "chacha_variant", 3),        # wave per record
+@pytest.mark.parametrize("alg,klen,opts", [
+    ("aesgcm", 16, {"gcm_variant": 16}),          # T-table lane per record
+    ("aesgcm", 32, {"gcm_variant": 16}),
+    ("aesgcm", 16, {"gcm_variant": 6}),           # wave per record
+    ("aesgcm", 32, {"gcm_variant": 6}),
+    ("aesgcm", 16, {"gcm_variant": 14}),          # 8-block bitsliced, octet per record
+    ("aesgcm", 32, {"gcm_variant": 14}),
+    ("aesgcm", 16, {"gcm_variant": 15}),          # hybrid T-table + bitsliced (persistent)
+    ("aesgcm", 32, {"gcm_variant": 15}),
+    ("aesgcm", 16, {"gcm_variant": 15, "hy_threads": 768}),   # 3 waves / SIMD, payload prefetch
+    ("aesgcm", 32, {"gcm_variant": 15, "hy_threads": 768}),
+    ("chacha", 32, {"chacha_variant": 4}),        # lane per record
+    ("chacha", 32, {"chacha_variant": 3}),        # wave per record
 ])
 @pytest.mark.parametrize("align", [16, 1])
-def test_forced_kernel_vs_oracle(torch, tg, oracle_mod, alg, klen, opt, value, align):
+def test_forced_kernel_vs_oracle(torch, tg, oracle_mod, alg, klen, opts, align):
     from batchpack import HostBatch, run_seal_open
-    rng = np.random.default_rng(hash((alg, klen, value, align)) & 0xffff)
+    rng = np.random.default_rng(hash((alg, klen, tuple(sorted(opts.items())), align)) & 0xffff)
     # + long records: many 256-counter windows (window-cache refreshes)
     lens = LENS * 5 + list(rng.integers(0, 16401, 120)) + [65520, 65536, 70001]
     hb = HostBatch(lens, payload_seed=align + 21, align=align, aad_mode="random")
     key = rng.bytes(klen)
     obj = tg.HipAESGCM(bytearray(key)) if alg == "aesgcm" else tg.HipCHACHA20_POLY1305(bytearray(key))
-    with tg.options(**{opt: value}):
+    with tg.options(**opts):
         run_seal_open(torch, tg, oracle_mod, hb, alg, np.frombuffer(key, np.uint8), obj,
                       tamper=(1, 30, 111))
 
@@ -171,28 +173,37 @@ def test_key_table_wave_kernel(torch, tg, oracle_mod, klen, align):
 @pytest.mark.parametrize("klen", [16, 32])
 @pytest.mark.parametrize("keys", [2, 37, 300])
 @pytest.mark.parametrize("align", [16, 1])
-@pytest.mark.parametrize("variant,split", [(14, 0), (0, 0), (0, 1000), (0, 4097)])
-def test_key_table_octet_kernel(torch, tg, oracle_mod, klen, keys, align, variant, split):
+@pytest.mark.parametrize("variant,split,lpr", [(14, 0, 0), (0, 0, 8), (0, 1000, 8), (0, 4097, 8),
+                                              (0, 0, 16), (0, 1000, 32), (0, 4097, 64), (0, 0, 64),
+                                              (6, 0, 0), (0, 1000, -1), (0, 4097, -1)])
+def test_key_table_octet_kernel(torch, tg, oracle_mod, klen, keys, align, variant, split, lpr):
     """Many keys, ragged lengths, through the key-grouped octet kernel
     (aes_gcm_bs8.hip gcm_kt_kernel): jobs of at most eight records of one
     key, bitsliced keystream with the key's planes, GHASH through the wave's
     4-bit tables of the key's H^8.  Variant 14 sends every record there; the
     auto path (0) splits the batch by length at kt_split (0 = the default
-    2048) and runs the shorter records through the lane kernel from the
-    tail of the same plan."""
+    2048), runs the long ones through the key-grouped bitsliced kernel with
+    kt_lpr = 8 / 16 / 32 / 64 lanes per record (jobs of 8 / 4 / 2 / 1 records
+    of one key, GHASH stride H^lpr) or the wave-per-record T-table kernel with
+    per-wave 4-bit GHASH tables (kt_lpr -1), and the shorter records through
+    the lane kernel from the tail of the same plan; variant 6 sends every
+    record to the wave-per-record kernel."""
     from batchpack import HostBatch, run_seal_open
-    rng = np.random.default_rng(700 + klen + keys + align + split)
+    rng = np.random.default_rng(700 + klen + keys + align + split + lpr)
     lens = LENS * 4 + list(rng.integers(0, 16401, 400)) + [999, 1000, 1001, 2047, 2048, 2049,
                                                             4096, 4097, 20000, 65000, 70001]
     hb = HostBatch(lens, payload_seed=align + 91, align=align, aad_mode="random", key_count=keys)
     kb = [rng.bytes(klen) for _ in range(keys)]
     obj = tg.KeyTable("aesgcm", kb)
     karr = np.frombuffer(b"".join(kb), np.uint8).reshape(keys, klen)
-    with tg.options(gcm_table_variant=variant, kt_split=split):
+    with tg.options(gcm_table_variant=variant, kt_split=split, kt_lpr=lpr):
         run_seal_open(torch, tg, oracle_mod, hb, "aesgcm", karr, obj, tamper=(4, 100, len(lens) - 1))
 
 
 @pytest.mark.parametrize("alg,opts", [("aesgcm", {"gcm_table_variant": 0}),
+                                      ("aesgcm", {"gcm_table_variant": 0, "kt_lpr": -1}),
+                                      ("aesgcm", {"gcm_table_variant": 0, "kt_lpr": 32}),
+                                      ("aesgcm", {"gcm_table_variant": 6}),
                                       ("aesgcm", {"gcm_table_variant": 1}),
                                       ("aesgcm", {"gcm_table_variant": 5}),
                                       ("aesgcm", {"gcm_table_variant": 14}),

@@ -139,31 +139,36 @@ TG_BS_HD uint32_t rec_plane(const uint32_t u[4], int e) {
            (bs::bitmask(u[2], e) & 0x00ff0000u) | (bs::bitmask(u[3], e) & 0xff000000u);
 }
 
-// Per-lane counter constants for c0 = the lane's first counter (< 64):
-// counter bits 0..5 of block j are those of c0 + 8 j (no carry out of bit 5
-// except into the batch bits, see ctr_planes), as byte-3 planes lane[b] of
-// row 3; kmask = ~0 when c0 >= 8 (block 7 then carries into bit 6).
-TG_BS_HD void lane_consts(uint32_t c0, uint32_t lane[6], uint32_t& kmask) {
+// Per-lane counter constants: block j of a lane's batch has counter
+// c0 + (j << SB) (SB = 3 for eight lanes per record: blocks 8 apart; 4 / 5 /
+// 6 for 16 / 32 / 64 lanes), c0 = the lane's first counter.  Counter bits
+// 0 .. SB + 2 differ per block j but not per batch: lane[b] is their
+// byte-3 plane for bit b (bits 0..7 belong to row 3, bit 8 to row 2); no
+// carry leaves them except out of block 7 into the batch bits when
+// c0 mod 2^(SB+3) >= 2^SB, which kmask = ~0 marks (see ctr_planes).
+template <int SB = 3>
+TG_BS_HD void lane_consts(uint32_t c0, uint32_t (&lane)[SB + 3], uint32_t& kmask) {
 #pragma unroll
-    for (int b = 0; b < 6; ++b) {
+    for (int b = 0; b < SB + 3; ++b) {
         uint32_t m = 0;
 #pragma unroll
-        for (int j = 0; j < 8; ++j) m |= (((c0 + 8u * j) >> b) & 1u) << j;
+        for (int j = 0; j < 8; ++j) m |= (((c0 + ((uint32_t)j << SB)) >> b) & 1u) << j;
         lane[b] = m << 24;
     }
-    kmask = (c0 >> 3) & 1u ? 0xffffffffu : 0u;
+    kmask = (c0 >> SB) & 1u ? 0xffffffffu : 0u;
 }
 
-// XOR the batch part of the counters (bits p >= 6: beta, or beta + 1 for
-// block 7 of lanes with kmask) into the state, for counter bits [P0, P1).
-// The kernel does bits 6..15 (rows 3 and 2) every batch and bits 16..31 only
-// once beta + 1 >= 2^10 (records over 1 MiB; a wave-uniform test).
-template <int P0, int P1>
+// XOR the batch part of the counters (bits p >= Q0 = SB + 3: beta, or
+// beta + 1 for block 7 of lanes with kmask) into the state, for counter bits
+// [P0, P1).  The kernel does bits Q0..15 (rows 3 and 2) every batch and bits
+// 16..31 only once beta + 1 >= 2^(16 - Q0) (records over 1 MiB for eight
+// lanes per record; a wave-uniform test).
+template <int P0, int P1, int Q0 = 6>
 TG_BS_HD void ctr_planes(uint32_t (*s)[8], uint32_t kmask, uint32_t beta) {
     const uint32_t flip = beta ^ (beta + 1u);
 #pragma unroll
     for (int p = P0; p < P1; ++p) {
-        const uint32_t q = (uint32_t)(p - 6);
+        const uint32_t q = (uint32_t)(p - Q0);
         const uint32_t A = ((beta >> q) & 1u) ? 0xff000000u : 0u;
         const uint32_t D = ((flip >> q) & 1u) ? 0x80000000u : 0u;
         uint32_t& r = s[3 - (p >> 3)][p & 7];

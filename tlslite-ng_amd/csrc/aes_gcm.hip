@@ -472,15 +472,19 @@ int launch_table_v(const GcmTableKey* keys, uint64_t nkeys, const tg_batch& b, h
 // config 4).  Wave w of the workgroup seals / opens record i with key
 // key_idx[i]: the index is wave-uniform, so the round keys are scalar loads
 // into SGPRs (no VGPRs, no LDS rows).  The layout is the single-key wave
-// kernel's with W = 1 (lane l takes blocks l, l + 64, ...: coalesced), but
-// GHASH is the table-free multiply: Horner with stride H^64 and one lift by
-// H^(64 - l), both read from the key's 64 precomputed powers
-// (hpow[64 k + e - 1] = H^e, built at key setup by table_hpow_kernel).
-// No length planning: a wave takes as long as its own record.
-template <int NR, bool OPEN>
+// kernel's with W = 1 (lane l takes blocks l, l + 64, ...: coalesced);
+// GHASH is Horner with stride H^64 and one lift by H^(64 - l), from the
+// key's 64 precomputed powers (hpow[64 k + e - 1] = H^e, built at key setup
+// by table_hpow_kernel).  T4: the stride multiply goes through 4-bit tables
+// of the record's H^64 that the wave builds in its own 8 KiB of LDS at
+// ``tab`` (ghash.h build_table4 / gmul4: 32 conflict-free lookups instead
+// of the table-free multiply's ~650 VALU slots; ~700 VALU per lane to build,
+// i.e. ~45 per block of a 16 KiB record); otherwise the table-free multiply.
+template <int NR, bool OPEN, bool T4>
 __device__ __forceinline__ void gcm_table_wave_record(const GcmTableKey* __restrict__ keys,
                                                       uint64_t nkeys, const uint4* __restrict__ hpow,
-                                                      const tg_batch& b, uint64_t i, uint32_t lane) {
+                                                      const tg_batch& b, uint64_t i, uint32_t lane,
+                                                      uint32_t tab, uint32_t& tab_key) {
     const uint32_t ki = (uint32_t)__builtin_amdgcn_readfirstlane((int)(b.key_idx ? b.key_idx[i] : 0u));
     if (ki >= nkeys) {   // out-of-range key index: skipped (open: rejected)
         if (OPEN && b.status && lane == 0) b.status[i] = 0;
@@ -492,6 +496,11 @@ __device__ __forceinline__ void gcm_table_wave_record(const GcmTableKey* __restr
     for (int k = 0; k < 4 * (NR + 1); ++k) rk.w[k] = kp->rk[k];
     const uint4* hp = hpow + 64ull * ki;
     const uint4 h64 = hp[63];
+    if (T4 && ki != tab_key) {   // this wave's tables of H^64 (kept while the key repeats)
+        build_table4(tab, h64);
+        __builtin_amdgcn_wave_barrier();
+        tab_key = ki;
+    }
     const uint32_t lane4 = (lane & 31u) << 2;
     const uint8_t* in = rec_in(b, i);
     uint8_t* out = rec_out(b, i);
@@ -509,7 +518,8 @@ __device__ __forceinline__ void gcm_table_wave_record(const GcmTableKey* __restr
     uint4 wc = make_uint4(0, 0, 0, 0);         // 256-counter window cache (aes_round.h)
     uint32_t whi = 0xffffffffu;
     for (uint32_t j = 0; j < Bw; ++j) {
-        if (j) y = gf128_mul(y, h64);           // y H^64 (wave-uniform)
+        // y H^64 (T4: y in block byte layout, else normal order)
+        if (j) y = T4 ? gmul4(y, tab) : gf128_mul(y, h64);
         const uint32_t t = 64 * j + lane;
         if (t < pad) continue;                  // leading zero blocks
         const uint32_t k = t - pad;
@@ -539,8 +549,9 @@ __device__ __forceinline__ void gcm_table_wave_record(const GcmTableKey* __restr
             x = make_uint4(bswap32((uint32_t)(abits >> 32)), bswap32((uint32_t)abits),
                            bswap32((uint32_t)(cbits >> 32)), bswap32((uint32_t)cbits));
         }
-        y = xor4(y, norm4(x));
+        y = xor4(y, T4 ? x : norm4(x));
     }
+    if (T4) y = norm4(y);
     if (y.x | y.y | y.z | y.w) y = gf128_mul(y, hp[63 - lane]);   // lift by H^(64 - l)
 #pragma unroll
     for (int m = 1; m < 64; m <<= 1) y = xor4(y, shfl_xor4(y, m));
@@ -565,32 +576,45 @@ __device__ __forceinline__ void gcm_table_wave_record(const GcmTableKey* __restr
     }
 }
 
-// A persistent grid (two workgroups per CU): wave g takes records g, g + G,
-// g + 2G, ... so a workgroup's waves finish together however the lengths mix
-// (one workgroup per record group would hold its LDS until its longest
-// record is done).  768 threads: two workgroups (2 x 64 KiB of T-tables) per
-// CU (512 / 1024 measured no better, profiles/r01/v24_c4_*.json).
-constexpr int kTwThreads = 768;
+// A persistent grid: wave g takes plan slots g, g + G, g + 2G, ... of
+// [0, count) (count: NULL = all n records; order: NULL = identity), so a
+// workgroup's waves finish together however the lengths mix (one workgroup
+// per record group would hold its LDS until its longest record is done).
+// Table-free GHASH: 768 threads, two workgroups (2 x 64 KiB of T-tables) per
+// CU (512 / 1024 measured no better, profiles/r01/v24_c4_*.json).  T4: 512
+// threads, one workgroup per CU: 64 KiB of T-tables + 8 KiB of GHASH tables
+// per wave.
+template <bool T4>
+constexpr int tw_threads() { return T4 ? 512 : 768; }
+template <bool T4>
+constexpr int tw_lds() { return 65536 + (T4 ? 8192 * (tw_threads<T4>() / 64) : 0); }
 
-template <int NR, bool OPEN>
-__global__ __launch_bounds__(kTwThreads) void gcm_table_wave_kernel(
-    const GcmTableKey* __restrict__ keys, uint64_t nkeys, const uint4* __restrict__ hpow, tg_batch b) {
+template <int NR, bool OPEN, bool T4>
+__global__ __launch_bounds__(tw_threads<T4>()) void gcm_table_wave_kernel(
+    const GcmTableKey* __restrict__ keys, uint64_t nkeys, const uint4* __restrict__ hpow, tg_batch b,
+    const uint32_t* __restrict__ order, const uint32_t* __restrict__ count) {
+    constexpr int kW = tw_threads<T4>() / 64;
     stage_te(reinterpret_cast<uint32_t*>(g_lds));   // Te0/Te2 copies at LDS 0
     __syncthreads();
-    const uint64_t G = (uint64_t)gridDim.x * (kTwThreads / 64);
+    const uint64_t G = (uint64_t)gridDim.x * kW;
+    const uint64_t nslots = count ? *count : b.n;
     const uint32_t wave = (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
-    for (uint64_t i = (uint64_t)blockIdx.x * (kTwThreads / 64) + wave; i < b.n; i += G)
-        gcm_table_wave_record<NR, OPEN>(keys, nkeys, hpow, b, i, threadIdx.x & 63u);
+    const uint32_t tab = 65536u + 8192u * wave;
+    uint32_t tab_key = 0xffffffffu;
+    for (uint64_t t = (uint64_t)blockIdx.x * kW + wave; t < nslots; t += G)
+        gcm_table_wave_record<NR, OPEN, T4>(keys, nkeys, hpow, b, order ? gld(order, t) : t, threadIdx.x & 63u,
+                                            tab, tab_key);
 }
 
-template <int NR, bool OPEN>
+template <int NR, bool OPEN, bool T4>
 int launch_table_wave(const GcmTableKey* keys, uint64_t nkeys, const uint4* hpow, const tg_batch& b,
-                      hipStream_t s) {
-    if (lds_attr((const void*)gcm_table_wave_kernel<NR, OPEN>, 65536)) return TG_EHIP;
-    const uint64_t groups = (b.n + kTwThreads / 64 - 1) / (kTwThreads / 64);
-    const uint64_t cap = 2ull * (uint64_t)device_cus();
-    hipLaunchKernelGGL((gcm_table_wave_kernel<NR, OPEN>), dim3((unsigned)(groups < cap ? groups : cap)),
-                       dim3(kTwThreads), 65536, s, keys, nkeys, hpow, b);
+                      hipStream_t s, const uint32_t* order, const uint32_t* count) {
+    constexpr int thr = tw_threads<T4>(), lds = tw_lds<T4>();
+    if (lds_attr((const void*)gcm_table_wave_kernel<NR, OPEN, T4>, lds)) return TG_EHIP;
+    const uint64_t groups = (b.n + thr / 64 - 1) / (thr / 64);
+    const uint64_t cap = (T4 ? 1ull : 2ull) * (uint64_t)device_cus();
+    hipLaunchKernelGGL((gcm_table_wave_kernel<NR, OPEN, T4>), dim3((unsigned)(groups < cap ? groups : cap)),
+                       dim3(thr), lds, s, keys, nkeys, hpow, b, order, count);
     return hipGetLastError() == hipSuccess ? TG_OK : TG_EHIP;
 }
 
@@ -688,13 +712,21 @@ int tg_launch_gcm_table_lane(const tg::GcmTableKey* keys, uint64_t nkeys, int ro
 }
 
 int tg_launch_gcm_table_wave(const tg::GcmTableKey* keys, uint64_t nkeys, const uint4* hpow, int rounds,
-                             const tg_batch& b, bool open, hipStream_t s) {
-    if (rounds == 10)
-        return open ? tg::launch_table_wave<10, true>(keys, nkeys, hpow, b, s)
-                    : tg::launch_table_wave<10, false>(keys, nkeys, hpow, b, s);
-    if (rounds == 14)
-        return open ? tg::launch_table_wave<14, true>(keys, nkeys, hpow, b, s)
-                    : tg::launch_table_wave<14, false>(keys, nkeys, hpow, b, s);
+                             const tg_batch& b, bool open, hipStream_t s, bool t4, const uint32_t* order,
+                             const uint32_t* count) {
+#define TG_TW(NR, OP, T)                                                                           \
+    return tg::launch_table_wave<NR, OP, T>(keys, nkeys, hpow, b, s, order, count)
+    if (rounds == 10) {
+        if (open) { if (t4) TG_TW(10, true, true); TG_TW(10, true, false); }
+        if (t4) TG_TW(10, false, true);
+        TG_TW(10, false, false);
+    }
+    if (rounds == 14) {
+        if (open) { if (t4) TG_TW(14, true, true); TG_TW(14, true, false); }
+        if (t4) TG_TW(14, false, true);
+        TG_TW(14, false, false);
+    }
+#undef TG_TW
     return TG_EINVAL;
 }
 

@@ -155,15 +155,24 @@ struct TableKeyCtx {    // a key of a key table: the wave's 4-bit H^8 tables in 
 // T-table cipher (aes_round.h, Te tables at kTeBase, round keys in SGPRs)
 // instead of the bitsliced one; everything else is shared.  ``recb``: this
 // wave's 1 KiB of LDS for the records' first-state planes.
-template <int NR, bool OPEN, bool TROLE, class KM, class KC, bool PRE = false>
+// LPR (lanes per record, 8 / 16 / 32 / 64; bitsliced only above 8): the same
+// job with a group of LPR lanes per record and 64 / LPR records per wave --
+// lane l of a group owns the GHASH positions l, l + LPR, ... (stride H^LPR:
+// kc.gmul multiplies by H^LPR), batch beta of the lane holds its blocks
+// rho + LPR (8 beta + j), j = 0..7, so each load / store instruction still
+// moves LPR x 16 consecutive bytes per record (whole 128-byte lines).
+template <int NR, bool OPEN, bool TROLE, class KM, class KC, bool PRE = false, int LPR = 8>
 __device__ __forceinline__ void octet_job(const KC& kc, const tg_batch& b,
                                           const uint32_t* __restrict__ order, uint64_t t0,
                                           uint32_t recw, const RkLds& rkT, uint32_t sbox,
                                           const KM& km) {
+    static_assert(LPR == 8 || LPR == 16 || LPR == 32 || LPR == 64, "lanes per record");
+    static_assert(LPR == 8 || !TROLE, "the T-table role runs octets only");
+    constexpr uint32_t kM = LPR - 1, kS = LPR == 8 ? 3 : LPR == 16 ? 4 : LPR == 32 ? 5 : 6;
     const uint32_t* rk = kc.rk();
     const uint32_t lane = threadIdx.x & 63u;
-    const uint32_t l = lane & 7u;
-    const uint64_t t = t0 + (lane >> 3);
+    const uint32_t l = lane & kM;
+    const uint64_t t = t0 + (lane >> kS);
     const bool valid = t < b.n;
     const uint64_t i = valid ? (order ? gld(order, t) : t) : 0;
     uint32_t len = 0, alen = 0;
@@ -180,22 +189,23 @@ __device__ __forceinline__ void octet_job(const KC& kc, const tg_batch& b,
         nv = load_partial(b.nonce + 12 * i, 12);
     }
     const uint32_t nfull = len >> 4, tail = len & 15, nc = (len + 15) >> 4, na = (alen + 15) >> 4;
-    const uint32_t rho = (l + nc + 1u) & 7u;   // this lane's ciphertext blocks: rho + 8 v
-    const uint32_t recb = recw + (lane >> 3) * 128u;
+    const uint32_t rho = (l + nc + 1u) & kM;   // this lane's ciphertext blocks: rho + LPR v
+    const uint32_t recb = recw + (lane >> kS) * 128u;
     const uint32_t lane4 = ((lane & 31u) << 2) | kTeBase;
     CtrCache cc = {0, 0, 0, 0};
     if (TROLE) {
         cc = ctr_cache<NR>(lane4, rkT, nv);
     } else {   // the record's first-state planes 4 l .. 4 l + 3 (nonce ^ rk0 spread to bytes)
         const uint32_t u[4] = {nv.x ^ rk[0], nv.y ^ rk[1], nv.z ^ rk[2], rk[3]};
-        const uint4 rp = make_uint4(bs8::rec_plane(u, 4 * l), bs8::rec_plane(u, 4 * l + 1),
-                                    bs8::rec_plane(u, 4 * l + 2), bs8::rec_plane(u, 4 * l + 3));
-        lds_st128(recb + 16u * l, rp);   // read back by the same wave (LDS is in order per wave)
+        const uint32_t e = 4 * (l & 7u);
+        const uint4 rp = make_uint4(bs8::rec_plane(u, e), bs8::rec_plane(u, e + 1),
+                                    bs8::rec_plane(u, e + 2), bs8::rec_plane(u, e + 3));
+        if (l < 8) lds_st128(recb + 16u * l, rp);   // read back by the same wave (in order per wave)
         __builtin_amdgcn_wave_barrier();
     }
     const bool aligned = (((uintptr_t)in | (uintptr_t)out) & 15) == 0;
-    const uint32_t nvl = nc > rho ? (nc - rho + 7u) >> 3 : 0u;          // blocks of this lane
-    const uint32_t nfl = nfull > rho ? (nfull - rho + 7u) >> 3 : 0u;    // full ones
+    const uint32_t nvl = nc > rho ? (nc - rho + kM) >> kS : 0u;         // blocks of this lane
+    const uint32_t nfl = nfull > rho ? (nfull - rho + kM) >> kS : 0u;   // full ones
     const uint32_t nbatch = wave_max_u32((nvl + 7u) >> 3);
     // batches in which every valid lane of the wave has all eight blocks full
     // (any alignment: the fast path's accesses are gload16u / gstore16u)
@@ -203,7 +213,7 @@ __device__ __forceinline__ void octet_job(const KC& kc, const tg_batch& b,
 
     // GHASH over this lane's AAD positions (aesgcm.py:69-79), zero-padded blocks
     uint4 y = make_uint4(0, 0, 0, 0);
-    for (uint32_t a = (l + na + nc + 1u) & 7u; a < na; a += 8) {
+    for (uint32_t a = (l + na + nc + 1u) & kM; a < na; a += LPR) {
         const uint32_t m = alen - 16 * a < 16 ? alen - 16 * a : 16;
         y = xor4(kc.gmul(y), load_partial(ad + 16 * a, m));
     }
@@ -217,18 +227,18 @@ __device__ __forceinline__ void octet_job(const KC& kc, const tg_batch& b,
     // pre: the slots' payload already loaded (fast path only), else nullptr
     auto consume = [&](const uint4* ks, uint32_t blk0, int j0, auto NN, const uint4* pre) {
         constexpr int N = decltype(NN)::value;
-        if (blk0 < (nfast << 6)) {   // every valid lane of the wave has these blocks full
+        if (blk0 < (nfast << (kS + 3))) {   // every valid lane of the wave has these blocks full
             if (valid) {
                 uint4 d[N];
 #pragma unroll
                 for (int q = 0; q < N; ++q)
-                    d[q] = pre ? pre[q] : gload16u(in + 16u * (blk0 + 8u * (j0 + q)));
+                    d[q] = pre ? pre[q] : gload16u(in + 16u * (blk0 + LPR * (j0 + q)));
 #pragma unroll
                 for (int q = 0; q < N; ++q) {
                     const uint4 k = ks[q];
                     const uint4 c = make_uint4(xor3(d[q].x, k.x, rkl.x), xor3(d[q].y, k.y, rkl.y),
                                                xor3(d[q].z, k.z, rkl.z), xor3(d[q].w, k.w, rkl.w));
-                    gstore16u(out + 16u * (blk0 + 8u * (j0 + q)), c);
+                    gstore16u(out + 16u * (blk0 + LPR * (j0 + q)), c);
                     if (!OPEN) d[q] = c;
                 }
 #pragma unroll
@@ -237,7 +247,7 @@ __device__ __forceinline__ void octet_job(const KC& kc, const tg_batch& b,
         } else {
 #pragma unroll
             for (int q = 0; q < N; ++q) {
-                const uint32_t blk = blk0 + 8u * (j0 + q);
+                const uint32_t blk = blk0 + LPR * (j0 + q);
                 if (!valid || blk >= nc) continue;
                 const uint4 k = ks[q];
                 const uint4 kk = make_uint4(k.x ^ rkl.x, k.y ^ rkl.y, k.z ^ rkl.z, k.w ^ rkl.w);
@@ -256,8 +266,8 @@ __device__ __forceinline__ void octet_job(const KC& kc, const tg_batch& b,
         }
     };
     for (uint32_t beta = 0; beta < nbatch; ++beta) {
-        const uint32_t blk0 = rho + 64u * beta;   // block of slot j: blk0 + 8 j
-        const uint32_t c0 = 2u + blk0;             // its counter: c0 + 8 j
+        const uint32_t blk0 = rho + 8u * LPR * beta;   // block of slot j: blk0 + LPR j
+        const uint32_t c0 = 2u + blk0;                  // its counter: c0 + LPR j
         // A batch in which no lane has more than one (four) of its blocks
         // left -- the last one of a record of 64 q + 1 blocks, e.g. a full TLS
         // 1.3 record's 16 385-byte inner plaintext -- runs one block per lane
@@ -303,21 +313,21 @@ __device__ __forceinline__ void octet_job(const KC& kc, const tg_batch& b,
                 s[q >> 1][4 * (q & 1) + 2] = v.z;
                 s[q >> 1][4 * (q & 1) + 3] = v.w;
             }
-            uint32_t lanec[6], kmask;
-            bs8::lane_consts(c0, lanec, kmask);
+            uint32_t lanec[kS + 3], kmask;
+            bs8::lane_consts<kS>(c0, lanec, kmask);
 #pragma unroll
-            for (int bb = 0; bb < 6; ++bb) s[3][bb] ^= lanec[bb];
-            bs8::ctr_planes<6, 16>(s, kmask, beta);
-            if ((beta + 1u) >> 10) bs8::ctr_planes<16, 32>(s, kmask, beta);
+            for (int bb = 0; bb < (int)kS + 3; ++bb) s[3 - (bb >> 3)][bb & 7] ^= lanec[bb];
+            bs8::ctr_planes<kS + 3, 16, kS + 3>(s, kmask, beta);
+            if ((beta + 1u) >> (16 - (kS + 3))) bs8::ctr_planes<16, 32, kS + 3>(s, kmask, beta);
             // PRE: the batch's payload is loaded before the cipher runs, so
             // the XOR does not wait for HBM (32 VGPRs live across encrypt():
             // only at three waves per SIMD; at four the seal kernel spilled
             // 270 registers)
             uint4 dp[8];
-            const bool pre = PRE && blk0 < (nfast << 6);
+            const bool pre = PRE && blk0 < (nfast << (kS + 3));
             if (pre && valid) {
 #pragma unroll
-                for (int q = 0; q < 8; ++q) dp[q] = gload16u(in + 16u * (blk0 + 8u * q));
+                for (int q = 0; q < 8; ++q) dp[q] = gload16u(in + 16u * (blk0 + LPR * q));
             }
             uint32_t w[4][8];
             bs8::encrypt<NR>(s, km, w);
@@ -329,16 +339,16 @@ __device__ __forceinline__ void octet_job(const KC& kc, const tg_batch& b,
     }
     if (!__any(valid)) return;
     // length block be64(8 alen) || be64(8 len) (aesgcm.py:64): the last position
-    if (l == 7) {
+    if (l == kM) {
         const uint64_t abits = (uint64_t)alen << 3, cbits = (uint64_t)len << 3;
         y = xor4(kc.gmul(y), make_uint4(bswap32((uint32_t)(abits >> 32)), bswap32((uint32_t)abits),
                                      bswap32((uint32_t)(cbits >> 32)), bswap32((uint32_t)cbits)));
     }
-    // lift by H^(8 - l) and XOR-reduce over the octet
+    // lift by H^(LPR - l) and XOR-reduce over the record's lanes
     uint4 yn = norm4(y);
-    if (yn.x | yn.y | yn.z | yn.w) yn = gf128_mul(yn, kc.hpow(8 - l));
+    if (yn.x | yn.y | yn.z | yn.w) yn = gf128_mul(yn, kc.hpow(LPR - l));
 #pragma unroll
-    for (int m = 1; m < 8; m <<= 1) yn = xor4(yn, shfl_xor4(yn, m));
+    for (int m = 1; m < LPR; m <<= 1) yn = xor4(yn, shfl_xor4(yn, m));
     // tag = GHASH ^ E_K(J0), J0 = nonce || be32(1) (aesgcm.py:112-122)
     if (valid) nv = load_partial(b.nonce + 12 * i, 12);   // reloaded: not held across the loop
     const uint4 mask = TROLE ? aes_ctr<NR>(lane4, rkT, cc, 1u)
@@ -356,11 +366,11 @@ __device__ __forceinline__ void octet_job(const KC& kc, const tg_batch& b,
         diff = (exp.x ^ tag.x) | (exp.y ^ tag.y) | (exp.z ^ tag.z) | (exp.w ^ tag.w);
         if (b.status) gst(b.status, i, (uint8_t)(diff == 0));
     }
-    diff = (uint32_t)__shfl((int)diff, (int)(lane & 56u), 64);
+    diff = (uint32_t)__shfl((int)diff, (int)(lane & ~kM & 63u), 64);
     if (valid && diff) {   // a rejected record's plaintext is zeroed: each lane its own blocks
         const uint4 z = make_uint4(0, 0, 0, 0);
-        for (uint32_t blk = rho; blk < nfull; blk += 8) store16(out + 16u * blk, z, aligned);
-        if (tail && (nfull & 7u) == rho) store_partial(out + 16u * nfull, z, tail);
+        for (uint32_t blk = rho; blk < nfull; blk += LPR) store16(out + 16u * blk, z, aligned);
+        if (tail && (nfull & kM) == rho) store_partial(out + 16u * nfull, z, tail);
     }
 }
 
@@ -488,15 +498,17 @@ int launch_bs8(const GcmKeyDev* key, const tg_batch& b, hipStream_t s, const uin
     return hipGetLastError() == hipSuccess ? TG_OK : TG_EHIP;
 }
 
-// Options hy_t (T-table waves per 16, default 8) and hy_noprio (1: the
-// T-table waves keep normal priority) are measurement knobs.
+// Options hy_t (T-table waves per workgroup, default half of them; -1 none)
+// and hy_noprio (1: the T-table waves keep normal priority) are measurement
+// knobs.
 template <int NR, bool OPEN>
 int launch_hy(const GcmKeyDev* key, const tg_batch& b, hipStream_t s, const uint32_t* order) {
     if ((b.n + 7) / 8 > 0xffffffffull) return TG_EINVAL;
     const int t = opt(kOptHyT);
     const bool small = opt(kOptHyThreads) == 768;
     const int waves = small ? 12 : 16;
-    const uint32_t nt = t > 0 && t <= waves ? (uint32_t)t : (uint32_t)waves / 2;
+    // t < 0: bitsliced waves only (measurement)
+    const uint32_t nt = t < 0 ? 0u : t > 0 && t <= waves ? (uint32_t)t : (uint32_t)waves / 2;
     const uint32_t prio = opt(kOptHyNoPrio) ? 0u : 1u;
     const void* fn = small ? (const void*)gcm_hy_kernel<NR, OPEN, 768> : (const void*)gcm_hy_kernel<NR, OPEN, 1024>;
     if (lds_attr(fn, (int)kHyLds)) return TG_EHIP;
@@ -547,7 +559,7 @@ constexpr uint32_t kKtRecBase = kKtSbox + 256;           // 1 KiB of record plan
 constexpr size_t kKtLds = kKtRecBase + kKtWaves * 1024;
 constexpr int kKtPlaneWords = 15 * 32;                   // per key in the plane table
 
-template <int NR, bool OPEN>
+template <int NR, bool OPEN, int LPR>
 __global__ __launch_bounds__(kKtThreads, 4) void gcm_kt_kernel(const GcmTableKey* __restrict__ keys,
                                                             const uint4* __restrict__ hpow,
                                                             const uint32_t* __restrict__ planes,
@@ -569,11 +581,12 @@ __global__ __launch_bounds__(kKtThreads, 4) void gcm_kt_kernel(const GcmTableKey
     if (p0 >= *nlong_p) return;
     const uint32_t k = (uint32_t)__builtin_amdgcn_readfirstlane((int)gld(b.key_idx, gld(order, p0)));
     const uint32_t tab = 8192u * wave, recw = kKtRecBase + wave * 1024u;
-    build_table4(tab, hpow[64u * k + 7u]);   // this wave's GHASH tables for the job's key
+    build_table4(tab, hpow[64u * k + LPR - 1u]);   // this wave's GHASH tables: the key's H^LPR
     __builtin_amdgcn_wave_barrier();
-    b.n = p1;   // the job's slots are p0 .. p1 - 1 (at most eight)
-    octet_job<NR, OPEN, false>(TableKeyCtx{keys[k].rk, hpow + 64u * k, tab}, b, order, p0, recw,
-                               RkLds{0}, kKtSbox, bs8::KeyPlanes{planes + kKtPlaneWords * k});
+    b.n = p1;   // the job's slots are p0 .. p1 - 1 (at most 64 / LPR)
+    octet_job<NR, OPEN, false, bs8::KeyPlanes, TableKeyCtx, false, LPR>(
+        TableKeyCtx{keys[k].rk, hpow + 64u * k, tab}, b, order, p0, recw, RkLds{0}, kKtSbox,
+        bs8::KeyPlanes{planes + kKtPlaneWords * k});
 }
 
 __global__ void kt_planes_kernel(const GcmTableKey* __restrict__ keys, uint64_t n, int nr,
@@ -586,20 +599,49 @@ __global__ void kt_planes_kernel(const GcmTableKey* __restrict__ keys, uint64_t 
 }
 
 // Key-table AES-GCM by record length (BASELINE config 4): records of at
-// least ``split`` bytes run the key-grouped octet kernel, the rest (and
+// least ``split`` bytes run the key-grouped octet kernel (long_kernel
+// kKtLongOctet) or the key-table wave-per-record kernel with per-wave 4-bit
+// GHASH tables (kKtLongWave, aes_gcm.hip), the rest (and
 // records whose key_idx is not below nkeys) the lane-per-record kernel
 // (aes_gcm.hip gcm_table_vkernel) over the tail of the same plan, which the
 // planner leaves sorted by length, longest first.  split 0: every in-range
 // record takes the octet kernel; split ~0u: every record the lane kernel.
+template <int NR, bool OPEN, int LPR>
+int launch_kt_jobs(const GcmTableKey* keys, uint64_t nkeys, const uint4* hpow, const uint32_t* planes,
+                   const tg_batch& b, hipStream_t s, const uint32_t* order, const uint32_t* jobpos,
+                   const uint32_t* njobs, const uint32_t* nlong) {
+    if (lds_attr((const void*)gcm_kt_kernel<NR, OPEN, LPR>, (int)kKtLds)) return TG_EHIP;
+    // jobs: at most ceil(c_k / R) per distinct key k of the long records (R =
+    // 64 / LPR records per job), i.e. n / R + min(n, nkeys), plus the tail's
+    // jobs (which exit at once)
+    constexpr uint64_t R = 64 / LPR;
+    const uint64_t maxjobs = (b.n + R - 1) / R + (nkeys < b.n ? nkeys : b.n) + 1;
+    const uint64_t groups = (maxjobs + kKtWaves - 1) / kKtWaves;
+    if (groups > 0x7fffffffull) return TG_EINVAL;
+    hipLaunchKernelGGL((gcm_kt_kernel<NR, OPEN, LPR>), dim3((unsigned)groups), dim3(kKtThreads), kKtLds, s, keys,
+                       hpow, planes, b, order, jobpos, njobs, nlong);
+    return hipGetLastError() == hipSuccess ? TG_OK : TG_EHIP;
+}
+
+// Key-table AES-GCM by record length (BASELINE config 4): records of at
+// least ``split`` bytes run the key-grouped bitsliced kernel with lpr lanes
+// per record (8: octet jobs of up to eight records of one key; 16 / 32 / 64:
+// jobs of 4 / 2 / 1) or, with lpr 0, the key-table wave-per-record kernel
+// with per-wave 4-bit GHASH tables (T-table AES, aes_gcm.hip); the rest (and
+// records whose key_idx is not below nkeys) the lane-per-record kernel
+// (aes_gcm.hip gcm_table_vkernel) over the tail of the same plan, which the
+// planner leaves sorted by length, longest first.  split 0: every in-range
+// record takes the long kernel; split ~0u: every record the lane kernel.
 template <int NR, bool OPEN>
 int launch_kt(const GcmTableKey* keys, uint64_t nkeys, const uint4* hpow, const uint32_t* planes,
-              const tg_batch& b, hipStream_t s, uint32_t split) {
-    if (lds_attr((const void*)gcm_kt_kernel<NR, OPEN>, (int)kKtLds)) return TG_EHIP;
+              const tg_batch& b, hipStream_t s, uint32_t split, int lpr) {
     if (b.n == 0) return TG_OK;
     if (b.n > 0xfffffffeull || !b.key_idx) return TG_EINVAL;
+    if (lpr != 0 && lpr != 8 && lpr != 16 && lpr != 32 && lpr != 64) return TG_EINVAL;
+    const uint32_t jobsz = lpr ? 64u / (uint32_t)lpr : 1u;
     size_t plan = 0;
-    int rc = tg_key_job_plan(b.key_idx, b.len, b.fixed_len, b.n, nkeys, split, nullptr, nullptr, nullptr,
-                             nullptr, nullptr, &plan, s);
+    int rc = tg_key_job_plan(b.key_idx, b.len, b.fixed_len, b.n, nkeys, split, jobsz, nullptr, nullptr,
+                             nullptr, nullptr, nullptr, &plan, s);
     if (rc) return rc;
     const size_t so = (b.n * 4 + 255) & ~(size_t)255, sj = ((b.n + 1) * 4 + 255) & ~(size_t)255;
     uint8_t* buf = nullptr;
@@ -608,17 +650,18 @@ int launch_kt(const GcmTableKey* keys, uint64_t nkeys, const uint4* hpow, const 
     uint32_t* jobpos = reinterpret_cast<uint32_t*>(buf + so);
     uint32_t* njobs = reinterpret_cast<uint32_t*>(buf + so + sj);
     uint32_t* nlong = njobs + 1;
-    rc = tg_key_job_plan(b.key_idx, b.len, b.fixed_len, b.n, nkeys, split, order, jobpos, njobs, nlong,
+    rc = tg_key_job_plan(b.key_idx, b.len, b.fixed_len, b.n, nkeys, split, jobsz, order, jobpos, njobs, nlong,
                          buf + so + sj + 256, &plan, s);
     if (!rc && split != 0xffffffffu) {
-        // jobs: at most ceil(c_k / 8) per distinct key k of the long records,
-        // i.e. n / 8 + min(n, nkeys), plus the tail's jobs (which exit at once)
-        const uint64_t maxjobs = (b.n + 7) / 8 + (nkeys < b.n ? nkeys : b.n) + 1;
-        const uint64_t groups = (maxjobs + kKtWaves - 1) / kKtWaves;
-        hipLaunchKernelGGL((gcm_kt_kernel<NR, OPEN>), dim3((unsigned)groups), dim3(kKtThreads), kKtLds, s,
-                           keys, hpow, planes, b, (const uint32_t*)order, (const uint32_t*)jobpos,
-                           (const uint32_t*)njobs, (const uint32_t*)nlong);
-        rc = hipGetLastError() == hipSuccess ? TG_OK : TG_EHIP;
+        switch (lpr) {
+            case 0:   // the long records one per wavefront (plan slots [0, nlong))
+                rc = tg_launch_gcm_table_wave(keys, nkeys, hpow, NR, b, OPEN, s, true, order, nlong);
+                break;
+            case 8: rc = launch_kt_jobs<NR, OPEN, 8>(keys, nkeys, hpow, planes, b, s, order, jobpos, njobs, nlong); break;
+            case 16: rc = launch_kt_jobs<NR, OPEN, 16>(keys, nkeys, hpow, planes, b, s, order, jobpos, njobs, nlong); break;
+            case 32: rc = launch_kt_jobs<NR, OPEN, 32>(keys, nkeys, hpow, planes, b, s, order, jobpos, njobs, nlong); break;
+            default: rc = launch_kt_jobs<NR, OPEN, 64>(keys, nkeys, hpow, planes, b, s, order, jobpos, njobs, nlong); break;
+        }
     }
     if (!rc) rc = tg_launch_gcm_table_lane(keys, nkeys, NR, b, OPEN, s, order, nlong);
     if (hipFreeAsync(buf, s) != hipSuccess) return TG_EHIP;
@@ -647,13 +690,13 @@ int tg_launch_gcm_bs8(const tg::GcmKeyDev* key, int rounds, const tg_batch& b, b
 }
 
 int tg_launch_gcm_kt(const tg::GcmTableKey* keys, uint64_t nkeys, const uint4* hpow, const uint32_t* planes,
-                     int rounds, const tg_batch& b, bool open, hipStream_t s, uint32_t split) {
+                     int rounds, const tg_batch& b, bool open, hipStream_t s, uint32_t split, int lpr) {
     if (rounds == 10)
-        return open ? tg::launch_kt<10, true>(keys, nkeys, hpow, planes, b, s, split)
-                    : tg::launch_kt<10, false>(keys, nkeys, hpow, planes, b, s, split);
+        return open ? tg::launch_kt<10, true>(keys, nkeys, hpow, planes, b, s, split, lpr)
+                    : tg::launch_kt<10, false>(keys, nkeys, hpow, planes, b, s, split, lpr);
     if (rounds == 14)
-        return open ? tg::launch_kt<14, true>(keys, nkeys, hpow, planes, b, s, split)
-                    : tg::launch_kt<14, false>(keys, nkeys, hpow, planes, b, s, split);
+        return open ? tg::launch_kt<14, true>(keys, nkeys, hpow, planes, b, s, split, lpr)
+                    : tg::launch_kt<14, false>(keys, nkeys, hpow, planes, b, s, split, lpr);
     return TG_EINVAL;
 }
 

@@ -197,25 +197,34 @@ int launch_kernels(tg_key* k, const tg_batch& b, bool open, hipStream_t s, const
     return tg_launch_chacha(static_cast<const tg::ChachaKeyDev*>(k->dev_key), k->nkeys, b, open, s, order);
 }
 
-// Key-table AES-GCM (option gcm_table_variant): 0 = auto (length split:
-// octet kernel for the long records, lane kernel for the rest, one plan);
-// 1 = the lane kernel for every record; 5 = the wave-per-record kernel;
-// 14 = the octet kernel for every record.
+// Key-table AES-GCM (option gcm_table_variant): 0 = auto (length split at
+// kt_split: the long records on the kernel kt_lpr picks -- 0 = default,
+// 8 / 16 / 32 / 64 lanes per record on the key-grouped bitsliced kernel, -1
+// the wave-per-record T-table kernel with 4-bit GHASH tables -- the rest on
+// the lane kernel, one plan); 1 = the lane kernel for every record; 5 = the
+// wave-per-record kernel, table-free GHASH, no plan; 6 = the wave-per-record
+// kernel with 4-bit tables for every record; 14 = the octet kernel (8 lanes
+// per record) for every record.
+constexpr int kKtLprDefault = 32;
+
 int launch_gcm_table(tg_key* k, const tg_batch& b, bool open, hipStream_t s) {
     const auto* keys = static_cast<const tg::GcmTableKey*>(k->dev_key);
     uint32_t split;
+    const int o = tg::opt(tg::kOptKtLpr);
+    int lpr = o == 0 ? kKtLprDefault : o < 0 ? 0 : o;
     switch (tg::opt(tg::kOptGcmTableVariant)) {
         case 0: {
-            const int o = tg::opt(tg::kOptKtSplit);
-            split = o > 0 ? (uint32_t)o : kKtSplitDefault;
+            const int sp = tg::opt(tg::kOptKtSplit);
+            split = sp > 0 ? (uint32_t)sp : kKtSplitDefault;
             break;
         }
         case 1: split = 0xffffffffu; break;
-        case 5: return tg_launch_gcm_table_wave(keys, k->nkeys, table_hpow(k), k->rounds, b, open, s);
-        case 14: split = 0; break;
+        case 5: return tg_launch_gcm_table_wave(keys, k->nkeys, table_hpow(k), k->rounds, b, open, s, false);
+        case 6: split = 0; lpr = 0; break;
+        case 14: split = 0; lpr = 8; break;
         default: return TG_EINVAL;
     }
-    return tg_launch_gcm_kt(keys, k->nkeys, table_hpow(k), table_planes(k), k->rounds, b, open, s, split);
+    return tg_launch_gcm_kt(keys, k->nkeys, table_hpow(k), table_planes(k), k->rounds, b, open, s, split, lpr);
 }
 
 // The order and the sort's scratch are allocated stream-ordered on the

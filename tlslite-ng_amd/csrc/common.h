@@ -259,24 +259,31 @@ int tg_launch_gcm_bs8(const tg::GcmKeyDev* key, int rounds, const tg_batch& b, b
 int tg_launch_table_hpow(const tg::GcmTableKey* keys, uint64_t n, uint4* hpow, hipStream_t s);
 int tg_length_order(const uint32_t* len, uint64_t n, uint32_t* order, void* scratch, size_t* bytes,
                     hipStream_t s);
-// Key-grouped octet jobs of a key-table batch (planner.hip): records of at
-// least ``split`` bytes with key_idx < nkeys in front, grouped by key; the
-// rest behind them from slot *nlong on, longest first.
+// Key-grouped jobs of a key-table batch (planner.hip): records of at least
+// ``split`` bytes with key_idx < nkeys in front, grouped by key and cut into
+// jobs of at most jobsz (a power of two) records of one key; the rest
+// behind them from slot *nlong on, longest first.
 int tg_key_job_plan(const uint32_t* key_idx, const uint32_t* len, uint32_t fixed_len, uint64_t n,
-                    uint64_t nkeys, uint32_t split, uint32_t* order, uint32_t* jobpos, uint32_t* njobs,
-                    uint32_t* nlong, void* scratch, size_t* bytes, hipStream_t s);
+                    uint64_t nkeys, uint32_t split, uint32_t jobsz, uint32_t* order, uint32_t* jobpos,
+                    uint32_t* njobs, uint32_t* nlong, void* scratch, size_t* bytes, hipStream_t s);
 // Key-table AES-GCM (aes_gcm_bs8.hip launch_kt): records of at least
 // ``split`` bytes through the key-grouped octet kernel (planes = per-key
 // bitsliced round-key planes, tg_launch_kt_planes; hpow = the keys'
 // H^1..H^64), the others through the lane kernel.
+// lpr: lanes per record of the key-grouped bitsliced kernel for the long
+// records (8, 16, 32 or 64), or 0 for the wave-per-record T-table kernel
+// with per-wave 4-bit GHASH tables.
 int tg_launch_gcm_kt(const tg::GcmTableKey* keys, uint64_t nkeys, const uint4* hpow, const uint32_t* planes,
-                     int rounds, const tg_batch& b, bool open, hipStream_t s, uint32_t split);
+                     int rounds, const tg_batch& b, bool open, hipStream_t s, uint32_t split, int lpr);
 // The key-table lane kernel over slots [*first, n) of ``order`` (first NULL:
 // all of them) and the key-table wave-per-record kernel (aes_gcm.hip).
 int tg_launch_gcm_table_lane(const tg::GcmTableKey* keys, uint64_t nkeys, int rounds, const tg_batch& b,
                              bool open, hipStream_t s, const uint32_t* order, const uint32_t* first);
+// t4: GHASH through per-wave 4-bit tables of H^64 (else table-free); plan
+// slots [0, *count) of ``order`` (NULL: every record, in order).
 int tg_launch_gcm_table_wave(const tg::GcmTableKey* keys, uint64_t nkeys, const uint4* hpow, int rounds,
-                             const tg_batch& b, bool open, hipStream_t s);
+                             const tg_batch& b, bool open, hipStream_t s, bool t4,
+                             const uint32_t* order = nullptr, const uint32_t* count = nullptr);
 int tg_launch_kt_planes(const tg::GcmTableKey* keys, uint64_t n, int rounds, uint32_t* planes,
                         hipStream_t s);
 int tg_launch_ccm(const tg::AesKeyDev* keys, uint64_t nkeys, int rounds, int taglen,

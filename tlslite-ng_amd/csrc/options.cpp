@@ -25,6 +25,7 @@ constexpr OptName kNames[kOptCount] = {
     {"hy_t", "TLSGPU_HY_T"},
     {"hy_noprio", "TLSGPU_HY_NOPRIO"},
     {"kt_split", "TLSGPU_KT_SPLIT"},
+    {"kt_lpr", "TLSGPU_KT_LPR"},
     {"hy_threads", "TLSGPU_HY_THREADS"},
 };
 

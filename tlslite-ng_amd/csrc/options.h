@@ -20,6 +20,8 @@ enum Opt {
     kOptHyT,                  // TLSGPU_HY_T: T-table waves of the hybrid kernel (0 = 8)
     kOptHyNoPrio,             // TLSGPU_HY_NOPRIO: 1 = T-table waves at normal priority
     kOptKtSplit,              // TLSGPU_KT_SPLIT: key-table length split in bytes, 0 = auto
+    kOptKtLpr,                // TLSGPU_KT_LPR: key-table long records, lanes per record
+                              // (8 / 16 / 32 / 64), -1 wave-per-record T-table, 0 auto
     kOptHyThreads,            // TLSGPU_HY_THREADS: hybrid AES-GCM workgroup, 0 = 1024, or 768
     kOptCount
 };

@@ -72,10 +72,11 @@ __global__ void kjp_group_starts(const uint64_t* __restrict__ ck, uint64_t n, ui
     g[t] = (t == 0 || (ck[t] >> 32) != (ck[t - 1] >> 32)) ? (uint32_t)t : 0u;
 }
 
-__global__ void kjp_job_starts(const uint32_t* __restrict__ gs, uint64_t n, uint32_t* __restrict__ js) {
+__global__ void kjp_job_starts(const uint32_t* __restrict__ gs, uint64_t n, uint32_t jobsz,
+                               uint32_t* __restrict__ js) {
     const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= n) return;
-    js[t] = (((uint32_t)t - gs[t]) & 7u) == 0 ? 1u : 0u;
+    js[t] = (((uint32_t)t - gs[t]) & (jobsz - 1u)) == 0 ? 1u : 0u;
 }
 
 __global__ void kjp_scatter(const uint32_t* __restrict__ js, const uint32_t* __restrict__ jx, uint64_t n,
@@ -96,11 +97,13 @@ size_t ru256(size_t v) { return (v + 255) & ~(size_t)255; }
 // scratch == nullptr: *bytes = what a batch of n needs.  Outputs: order[n]
 // (record index per slot), jobpos[n + 1] (first slot of job j; jobpos[njobs]
 // = n), *njobs and *nlong (device): slots [0, nlong) hold the records of at
-// least ``split`` bytes with key_idx < nkeys, grouped by key; slots
-// [nlong, n) the rest, longest first.  n < 2^32.
+// least ``split`` bytes with key_idx < nkeys, grouped by key, longest first
+// within a key, cut into jobs of at most jobsz records; slots [nlong, n) the
+// rest, longest first.  n < 2^32.
 int tg_key_job_plan(const uint32_t* key_idx, const uint32_t* len, uint32_t fixed_len, uint64_t n,
-                    uint64_t nkeys, uint32_t split, uint32_t* order, uint32_t* jobpos, uint32_t* njobs,
-                    uint32_t* nlong, void* scratch, size_t* bytes, hipStream_t s) {
+                    uint64_t nkeys, uint32_t split, uint32_t jobsz, uint32_t* order, uint32_t* jobpos,
+                    uint32_t* njobs, uint32_t* nlong, void* scratch, size_t* bytes, hipStream_t s) {
+    if (jobsz == 0 || (jobsz & (jobsz - 1u))) return TG_EINVAL;
     rocprim::counting_iterator<uint32_t> iota(0);
     size_t t_sort = 0, t_max = 0, t_sum = 0;
     if (rocprim::radix_sort_pairs(nullptr, t_sort, (uint64_t*)nullptr, (uint64_t*)nullptr, iota,
@@ -137,7 +140,7 @@ int tg_key_job_plan(const uint32_t* key_idx, const uint32_t* len, uint32_t fixed
     size_t tm = t_max;
     if (rocprim::inclusive_scan(t, tm, g, gs, (size_t)n, rocprim::maximum<uint32_t>(), s) != hipSuccess)
         return TG_EHIP;
-    hipLaunchKernelGGL(kjp_job_starts, dim3(blocks), dim3(256), 0, s, gs, n, js);
+    hipLaunchKernelGGL(kjp_job_starts, dim3(blocks), dim3(256), 0, s, gs, n, jobsz, js);
     uint32_t* jx = g;   // reused: the group starts are no longer needed
     size_t tp = t_sum;
     if (rocprim::inclusive_scan(t, tp, js, jx, (size_t)n, rocprim::plus<uint32_t>(), s) != hipSuccess)

@@ -1,6 +1,10 @@
 """Run each AEAD kernel once on a fixed batch, for rocprofv3 counter passes.
 
     rocprofv3 --pmc <counters> --output-format csv -d out -- python tools/prof_kernels.py
+
+PROF_RECORDS / PROF_LEN: batch shape (2^18 x 16 KiB); PROF_ALGS: which
+AEADs; PROF_OPTS: tlsgpu options as name=value,... (e.g. hy_t=16 for a
+hybrid kernel of T-table waves only, hy_t=-1 for bitsliced waves only).
 """
 import os
 import sys
@@ -18,6 +22,9 @@ def main():
     n = int(os.environ.get("PROF_RECORDS", 1 << 18))
     L = int(os.environ.get("PROF_LEN", 16384))
     algs = os.environ.get("PROF_ALGS", "aes128gcm,chacha20-poly1305").split(",")
+    for kv in filter(None, os.environ.get("PROF_OPTS", "").split(",")):
+        k, v = kv.split("=")
+        tlsgpu.set_option(k, int(v))
     inp = torch.randint(0, 256, (n * L,), dtype=torch.uint8, device="cuda")
     sealed = torch.empty(n * (L + 16), dtype=torch.uint8, device="cuda")
     back = torch.empty_like(inp)
@@ -34,7 +41,8 @@ def main():
                                                in_stride=L + 16, out_stride=L, fixed_aad_len=5,
                                                status=status))
         torch.cuda.synchronize()
-        assert int(status.sum()) == n
+        # PROF_NOCHECK=1: measurement builds whose output is not the AEAD's
+        assert os.environ.get("PROF_NOCHECK") == "1" or int(status.sum()) == n
     print("prof_kernels done", n, L, algs)
 
 
