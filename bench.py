@@ -170,7 +170,7 @@ def main():
                     help="CPU baseline: seconds each process seals/opens")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--e2e", action="store_true", help="also time the host<->device path")
-    ap.add_argument("--traffic-file", default=os.path.join(ROOT, "profiles", "r02", "traffic.json"),
+    ap.add_argument("--traffic-file", default=os.path.join(ROOT, "profiles", "r03", "traffic.json"),
                     help="per-launch HBM bytes from tools/traffic.sh (rocprofv3 FETCH_SIZE / "
                          "WRITE_SIZE passes at this config, calibrated per access shape) for "
                          "roofline.traffic")
@@ -377,6 +377,23 @@ def measured_traffic(path, kernel, n, L):
             "write_size_bytes": round(k["write_size_bytes"]), "access_shape": k["shape"],
             "fetch_factor": k["fetch_factor"], "write_factor": k["write_factor"],
             "traffic_over_algorithmic": round(k["hbm_bytes"] / algorithmic_bytes(n, L, kernel.rsplit("_", 1)[1]), 3),
+            "source": os.path.relpath(path, ROOT)}
+
+
+def c4_traffic(path, op):
+    """Config 4's HBM bytes per ``op`` (one seal or open of the whole batch:
+    the long-record and the short-record kernel together) from the
+    tools/traffic.sh summary, or None."""
+    if not os.path.exists(path):
+        return None
+    with open(path) as f:
+        ks = json.load(f).get("kernels", {})
+    parts = [ks.get("c4_kt_" + op), ks.get("c4_lane_" + op)]
+    if not all(parts):
+        return None
+    return {"hbm_bytes": round(sum(k["hbm_bytes"] for k in parts)),
+            "kernels": {"gcm_kt_kernel": round(parts[0]["hbm_bytes"]),
+                        "gcm_table_vkernel": round(parts[1]["hbm_bytes"])},
             "source": os.path.relpath(path, ROOT)}
 
 
@@ -673,6 +690,12 @@ def run_config4(args):
                          "unit": "GB/s", "frac": res[dom]["frac"], "frac_read": res[dom]["frac_read"],
                          "traffic": None},
             "verified": bool(ok)}
+    tr = c4_traffic(args.traffic_file, dom) if n == 1 << 20 and not args.c4_presorted else None
+    if tr:
+        alg = 2 * payload + n * (13 + NONCE_LEN + TAG_LEN + 4 + (1 if dom == "open" else 0))
+        tr["traffic_over_algorithmic"] = round(tr["hbm_bytes"] / alg, 3)
+        line["roofline"]["traffic"] = tr["hbm_bytes"]
+        line["roofline"]["traffic_detail"] = tr
     print(json.dumps(line), flush=True)
     if not ok:
         sys.exit(3)

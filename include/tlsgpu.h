@@ -70,7 +70,9 @@ int tg_init(int device);                   /* hipSetDevice for the calling threa
  *   kt_lpr             key-table long records: lanes per record of the
  *                      key-grouped bitsliced kernel (8 / 16 / 32 / 64; 0 =
  *                      32), -1 = the wave-per-record T-table kernel
- *   chacha_variant     0 auto, 3 wave per record, 4 lane per record
+ *   chacha_variant     0 auto, 3 wave per record, 4 lane per record with
+ *                      the register-staged tile, 5 lane per record with the
+ *                      LDS-DMA tile (auto's choice for large batches)
  *   ccm_variant        0 auto, 1 lane full rounds, 2 wave, 3 lane
  *   waves_per_record   0 auto, 1 / 4 / 16
  *   no_plan            1 = no length-sorted launch order

@@ -36,7 +36,8 @@ LENS = [0, 1, 15, 16, 17, 63, 64, 65, 1000, 1024, 1040, 4095, 16383, 16384, 1638
     ("aesgcm", 32, {"gcm_variant": 15}),
     ("aesgcm", 16, {"gcm_variant": 15, "hy_threads": 768}),   # 3 waves / SIMD, payload prefetch
     ("aesgcm", 32, {"gcm_variant": 15, "hy_threads": 768}),
-    ("chacha", 32, {"chacha_variant": 4}),        # lane per record
+    ("chacha", 32, {"chacha_variant": 4}),        # lane per record, register-staged tile fill
+    ("chacha", 32, {"chacha_variant": 5}),        # lane per record, LDS-DMA tile fill (auto)
     ("chacha", 32, {"chacha_variant": 3}),        # wave per record
 ])
 @pytest.mark.parametrize("align", [16, 1])
@@ -82,7 +83,8 @@ def test_auto_wave_per_record_batch(torch, tg, oracle_mod, alg, klen):
 @pytest.mark.parametrize("alg,klen,keys,opts", [
     ("aesgcm", 16, 1, {"gcm_variant": 16}), ("aesgcm", 16, 1, {"gcm_variant": 14}),
     ("aesgcm", 16, 1, {"gcm_variant": 15}), ("aesgcm", 32, 1, {"gcm_variant": 15}),
-    ("chacha", 32, 1, {"chacha_variant": 4}),
+    ("chacha", 32, 1, {"chacha_variant": 4}), ("chacha", 32, 1, {"chacha_variant": 5}),
+    ("chacha", 32, 29, {"chacha_variant": 4}),
     ("aesgcm", 32, 29, {"gcm_table_variant": 1}), ("aesgcm", 32, 29, {"gcm_table_variant": 0}),
     ("aesgcm", 16, 29, {"gcm_table_variant": 14}), ("chacha", 32, 29, {})])
 @pytest.mark.parametrize("align", [16, 1])
@@ -207,7 +209,8 @@ def test_key_table_octet_kernel(torch, tg, oracle_mod, klen, keys, align, varian
                                       ("aesgcm", {"gcm_table_variant": 1}),
                                       ("aesgcm", {"gcm_table_variant": 5}),
                                       ("aesgcm", {"gcm_table_variant": 14}),
-                                      ("chacha", {}), ("aesccm", {"ccm_variant": 2}),
+                                      ("chacha", {}), ("chacha", {"chacha_variant": 4}),
+                                      ("aesccm", {"ccm_variant": 2}),
                                       ("aesccm", {"ccm_variant": 3})])
 def test_key_index_out_of_range_is_skipped(torch, tg, oracle_mod, alg, opts):
     """A key-table record whose key_idx is not below the table's size is

@@ -184,14 +184,17 @@ def test_config1_digest(torch, tg):
 
 # ------------------------------------------- full-size (BASELINE configs 2/3)
 
-@pytest.mark.parametrize("alg", ["aesgcm", "chacha", "aesgcm-bs8"])
+@pytest.mark.parametrize("alg", ["aesgcm", "chacha", "aesgcm-bs8", "chacha-regs"])
 def test_full_size_roundtrip_and_samples(torch, tg, oracle_mod, alg):
     """2^20 x 16 KiB records: seal -> open round trip on the whole batch
     (size-independent property), and 64 sampled records bit-exact vs the oracle.
-    aesgcm-bs8 forces the 8-block bitsliced kernel (gcm_variant 14)."""
+    aesgcm-bs8 forces the 8-block bitsliced kernel (gcm_variant 14),
+    chacha-regs the register-staged tile fill (chacha_variant 4; the default
+    fills it by LDS-DMA)."""
     variant = 14 if alg == "aesgcm-bs8" else 0
-    alg = "aesgcm" if alg == "aesgcm-bs8" else alg
-    with tg.options(gcm_variant=variant):
+    cv = 4 if alg == "chacha-regs" else 0
+    alg = {"aesgcm-bs8": "aesgcm", "chacha-regs": "chacha"}.get(alg, alg)
+    with tg.options(gcm_variant=variant, chacha_variant=cv):
         _full_size(torch, tg, oracle_mod, alg)
 
 

@@ -100,16 +100,23 @@ __device__ __forceinline__ uint32_t wave_min(uint32_t v) {
 
 // Per-wave LDS: a 64-record x 128-byte tile -- row r = the record of lane r,
 // holding one aligned pair of 64-byte blocks (one 128-byte HBM line) -- and
-// the records' in/out base pointers.  The row's eight 16-byte chunks are
-// XOR-swizzled by (r >> 1) & 7, so both the row-wise accesses (16 lanes, 16
-// rows) and the coalesced ones (8 lanes per row) are bank-conflict-free.
+// the records' in/out base pointers.  Chunk c of row r sits at 16-byte slot
+// c ^ ((r >> 1) & 7) ^ 4 (r & 1): ds_read_b128 serves 16 lanes per LDS cycle
+// over the 16 slots of a 256-byte bank row (rows r and r + 1 share one) and
+// ds_write_b128 8 consecutive lanes over 8 slots of 128 bytes, so with this
+// swizzle the row-wise reads and writes (lane r, row r) and the coalesced
+// ones (8 lanes per row) are all conflict-free.  Round 2's c ^ ((r >> 1) & 7)
+// put lanes 2k and 2k + 1 of a row-wise write on one slot: 21 % of the LDS
+// cycles were bank conflicts (profiles/r02/v75/pmc_chacha_summary.txt).
 struct WaveTile {
     uint4 row[64][8];
     uint4 ptr[64];  // {in lo, in hi, out lo, out hi}
 };
 constexpr int kWavesPerGroup = kChachaThreads / 64;
 
-__device__ __forceinline__ uint32_t swz(uint32_t r, uint32_t c) { return c ^ ((r >> 1) & 7u); }
+__device__ __forceinline__ uint32_t swz(uint32_t r, uint32_t c) {
+    return c ^ ((r >> 1) & 7u) ^ ((r & 1u) << 2);
+}
 
 
 // Blocks [0, jmin) of all 64 records of a wave (every record has >= jmin full
@@ -246,10 +253,94 @@ __device__ __forceinline__ void tiled_blocks(WaveTile& t, uint32_t lane,
     if (jmin & 1u) store_pair(1, jmin - 1);
 }
 
+// tiled_blocks with the tile filled by LDS-DMA (global_load_lds_dwordx4): no
+// VGPR round trip and no ds_write for the loads.  A DMA instruction writes
+// 1 KiB lane-linearly (lane x -> slot x % 8 of row 8 q + x / 8), so the swizzle
+// goes on the source address: the lane landing in slot s of row r fetches
+// chunk s ^ ((r >> 1) & 7).  A group's next pair is fetched right after its
+// finished pair has been read out of the rows (after the row pass of the
+// iteration that completes it), so it has the next ChaCha block to land;
+// the wait for it is the first LDS read of the next iteration.
+template <bool OPEN>
+__device__ __forceinline__ void tiled_blocks_dma(WaveTile& t, uint32_t lane,
+                                                 const uint32_t (&k)[8], uint4 nv, uint32_t jmin,
+                                                 Poly32& p, uint32_t (&ks)[16]) {
+    const uint32_t grp = lane >> 5, cq = lane & 7u, rq = lane >> 3;
+    auto fetch_pair = [&](uint32_t g, uint32_t p0, const uint4 (&P)[4]) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const uint32_t r = 32 * g + 8 * q + rq;
+            const uint32_t c = swz(r, cq);          // the chunk that lands in slot cq
+            const uint32_t off = p0 + (c >> 2) < jmin ? 64 * p0 + 16 * c : 16 * (c & 3u);
+            const uint8_t* src = reinterpret_cast<const uint8_t*>(((uint64_t)P[q].y << 32) | P[q].x);
+            __builtin_amdgcn_global_load_lds(
+                (const __attribute__((address_space(1))) void*)(src + off),
+                (__attribute__((address_space(3))) void*)(&t.row[32 * g + 8 * q][0]),
+                16, 0, 0);
+        }
+    };
+    auto ptrs = [&](uint32_t g, uint4 (&P)[4]) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) P[q] = t.ptr[32 * g + 8 * q + rq];
+    };
+    // read group g's finished pair (blocks p0, p0 + 1), store it, fetch the next
+    auto turn = [&](uint32_t g, uint32_t p0) {
+        uint4 P[4], S[4];
+        ptrs(g, P);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const uint32_t r = 32 * g + 8 * q + rq;
+            S[q] = t.row[r][swz(r, cq)];
+        }
+        const uint32_t blk = p0 + (cq >> 2);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            uint8_t* dst = reinterpret_cast<uint8_t*>(((uint64_t)P[q].w << 32) | P[q].z);
+            if (blk < jmin && dst) gstore16(dst + 64 * p0 + 16 * cq, S[q]);
+        }
+        if (p0 + 2 < jmin) fetch_pair(g, p0 + 2, P);
+    };
+    {
+        uint4 P[4];
+        ptrs(0, P);
+        fetch_pair(0, 0, P);
+        ptrs(1, P);
+        fetch_pair(1, 0, P);
+    }
+    for (uint32_t i = 0; i <= jmin; ++i) {
+        const uint32_t b = i - grp;                 // this lane's block
+        const bool act = i >= grp && b < jmin;
+        uint4 m[4];
+        if (act) {
+            const uint32_t h = 4 * (b & 1u);
+            uint4 d[4];
+#pragma unroll
+            for (int c = 0; c < 4; ++c) d[c] = t.row[lane][swz(lane, h + c)];
+#pragma unroll
+            for (int c = 0; c < 4; ++c) {
+                const uint4 ct = make_uint4(d[c].x ^ ks[4 * c], d[c].y ^ ks[4 * c + 1], d[c].z ^ ks[4 * c + 2],
+                                            d[c].w ^ ks[4 * c + 3]);
+                t.row[lane][swz(lane, h + c)] = ct;
+                m[c] = OPEN ? d[c] : ct;
+            }
+        }
+        __builtin_amdgcn_wave_barrier();
+        // group A finished block i, group B block i - 1 (wave-uniform)
+        if (i < jmin && ((i & 1u) || i + 1 == jmin)) turn(0, i & ~1u);
+        if (i >= 1 && (((i - 1) & 1u) || i == jmin)) turn(1, (i - 1) & ~1u);
+        __builtin_amdgcn_wave_barrier();
+        if (act) {
+            chacha_block(k, b + 2, nv.x, nv.y, nv.z, ks);
+#pragma unroll
+            for (int c = 0; c < 4; ++c) poly_block(p, m[c]);
+        }
+    }
+}
+
 // A key-table record whose key_idx is not below nkeys is skipped (open:
 // status 0): its row still serves the wave's coalesced transfers, with its
 // output pointer cleared so the tile never stores it.
-template <bool OPEN, bool MULTIKEY, int MINW>
+template <bool OPEN, bool MULTIKEY, int MINW, bool DMA>
 __global__ __launch_bounds__(kChachaThreads, MINW) void chacha_kernel(
     const ChachaKeyDev* __restrict__ keys, uint64_t nkeys, tg_batch b, const uint32_t* __restrict__ order) {
     __shared__ WaveTile tiles[kWavesPerGroup];
@@ -315,7 +406,10 @@ __global__ __launch_bounds__(kChachaThreads, MINW) void chacha_kernel(
         t.ptr[lane] = make_uint4((uint32_t)(uintptr_t)tile_in, (uint32_t)((uintptr_t)tile_in >> 32),
                                  (uint32_t)(uintptr_t)tile_out, (uint32_t)((uintptr_t)tile_out >> 32));
         __builtin_amdgcn_wave_barrier();
-        tiled_blocks<OPEN>(t, lane, k, nv, jmin, p, ks);
+        if (DMA)
+            tiled_blocks_dma<OPEN>(t, lane, k, nv, jmin, p, ks);
+        else
+            tiled_blocks<OPEN>(t, lane, k, nv, jmin, p, ks);
         j0 = jmin;
     }
     if (valid) {
@@ -482,15 +576,21 @@ template <bool OPEN, bool MULTIKEY>
 int launch_w(const ChachaKeyDev* keys, uint64_t nkeys, const tg_batch& b, hipStream_t s, const uint32_t* order) {
     const uint64_t blocks = (b.n + kChachaThreads - 1) / kChachaThreads;
     if (blocks > 0x7fffffffull) return TG_EINVAL;
-    hipLaunchKernelGGL((chacha_kernel<OPEN, MULTIKEY, 4>), dim3((unsigned)blocks), dim3(kChachaThreads), 0, s,
-                       keys, nkeys, b, order);
+    if (opt(kOptChachaVariant) == 4)   // register-staged tile fill
+        hipLaunchKernelGGL((chacha_kernel<OPEN, MULTIKEY, 4, false>), dim3((unsigned)blocks), dim3(kChachaThreads),
+                           0, s, keys, nkeys, b, order);
+    else                                // LDS-DMA tile fill
+        hipLaunchKernelGGL((chacha_kernel<OPEN, MULTIKEY, 4, true>), dim3((unsigned)blocks), dim3(kChachaThreads),
+                           0, s, keys, nkeys, b, order);
     return hipGetLastError() == hipSuccess ? TG_OK : TG_EHIP;
 }
 
 // Option chacha_variant (tests and measurement): 0 = auto (wave per record
 // up to kWaveMaxRecords records, else lane per record at 4 waves per SIMD,
-// i.e. <= 128 VGPRs; 5 and 6 waves per SIMD measured slower), 3 = wave per
-// record, 4 = lane per record.
+// i.e. <= 128 VGPRs, tile filled by LDS-DMA; 5 and 6 waves per SIMD measured
+// slower), 3 = wave per record, 4 = lane per record with the register-staged
+// tile fill (1.5 % slower, profiles/r03/chacha_dma_nt_ab.txt), 5 = lane per
+// record (LDS-DMA fill).
 bool wave_path(uint64_t n) {
     const int v = opt(kOptChachaVariant);
     return v == 3 || (v == 0 && n <= kWaveMaxRecords);
@@ -499,7 +599,7 @@ bool wave_path(uint64_t n) {
 template <bool OPEN, bool MULTIKEY>
 int launch(const ChachaKeyDev* keys, uint64_t nkeys, const tg_batch& b, hipStream_t s, const uint32_t* order) {
     const int v = opt(kOptChachaVariant);
-    if (v != 0 && v != 3 && v != 4) return TG_EINVAL;
+    if (v != 0 && v != 3 && v != 4 && v != 5) return TG_EINVAL;
     if (!MULTIKEY && wave_path(b.n)) {
         // waves per record as in the GCM launcher (aes_gcm.hip waves_per_record)
         const int o = opt(kOptWavesPerRecord);

@@ -68,7 +68,11 @@ struct ChachaKeyDev {
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ uint4 gload16(const uint8_t* p) {
 #if defined(__HIP_DEVICE_COMPILE__)
+#if defined(TG_NT_IO)   // measurement build (tools/build_variant.sh): non-temporal record I/O
+    const u32x4 v = __builtin_nontemporal_load((const __attribute__((address_space(1))) u32x4*)p);
+#else
     const u32x4 v = *(const __attribute__((address_space(1))) u32x4*)p;
+#endif
     return make_uint4(v.x, v.y, v.z, v.w);
 #else
     return uint4();
@@ -76,7 +80,11 @@ __device__ __forceinline__ uint4 gload16(const uint8_t* p) {
 }
 __device__ __forceinline__ void gstore16(uint8_t* p, uint4 v) {
 #if defined(__HIP_DEVICE_COMPILE__)
+#if defined(TG_NT_IO)
+    __builtin_nontemporal_store(u32x4{v.x, v.y, v.z, v.w}, (__attribute__((address_space(1))) u32x4*)p);
+#else
     *(__attribute__((address_space(1))) u32x4*)p = u32x4{v.x, v.y, v.z, v.w};
+#endif
 #endif
 }
 

@@ -50,12 +50,12 @@ def loops(body):
         m = re.match(r"^(\.LBB[\w_]+):", l)
         if m:
             labels[m.group(1)] = i
-    out = []
+    last = {}   # loop header -> its last backward branch (one loop per header)
     for i, l in enumerate(body):
         m = re.match(r"^\s+s_(cbranch_\w+|branch)\s+(\.LBB[\w_]+)", l)
         if m and m.group(2) in labels and labels[m.group(2)] < i:
-            out.append((labels[m.group(2)], i))
-    return out
+            last[labels[m.group(2)]] = i
+    return sorted(last.items())
 
 
 def classify(line):

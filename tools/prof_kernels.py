@@ -2,9 +2,11 @@
 
     rocprofv3 --pmc <counters> --output-format csv -d out -- python tools/prof_kernels.py
 
-PROF_RECORDS / PROF_LEN: batch shape (2^18 x 16 KiB); PROF_ALGS: which
-AEADs; PROF_OPTS: tlsgpu options as name=value,... (e.g. hy_t=16 for a
-hybrid kernel of T-table waves only, hy_t=-1 for bitsliced waves only).
+PROF_RECORDS / PROF_LEN: batch shape (2^18 x 16 KiB); sealed records at
+bench.py's 128-byte aligned stride; PROF_REPS: seal + open rounds (1);
+PROF_ALGS: which AEADs; PROF_OPTS: tlsgpu options as name=value,... (e.g.
+hy_t=16 for a hybrid kernel of T-table waves only, hy_t=-1 for bitsliced
+waves only).
 """
 import os
 import sys
@@ -25,8 +27,10 @@ def main():
     for kv in filter(None, os.environ.get("PROF_OPTS", "").split(",")):
         k, v = kv.split("=")
         tlsgpu.set_option(k, int(v))
+    reps = int(os.environ.get("PROF_REPS", 1))
+    so = (L + 16 + 127) // 128 * 128
     inp = torch.randint(0, 256, (n * L,), dtype=torch.uint8, device="cuda")
-    sealed = torch.empty(n * (L + 16), dtype=torch.uint8, device="cuda")
+    sealed = torch.empty(n * so, dtype=torch.uint8, device="cuda")
     back = torch.empty_like(inp)
     status = torch.zeros(n, dtype=torch.uint8, device="cuda")
     nonces = torch.empty(12 * n, dtype=torch.uint8, device="cuda")
@@ -35,11 +39,12 @@ def main():
     for a in algs:
         c = tlsgpu.HipAESGCM(bytearray(16)) if a == "aes128gcm" else \
             tlsgpu.HipCHACHA20_POLY1305(bytearray(32))
-        tlsgpu.seal_batch(c, tlsgpu.make_batch(n, inp, sealed, nonces, aad=aad, fixed_len=L,
-                                               in_stride=L, out_stride=L + 16, fixed_aad_len=5))
-        tlsgpu.open_batch(c, tlsgpu.make_batch(n, sealed, back, nonces, aad=aad, fixed_len=L,
-                                               in_stride=L + 16, out_stride=L, fixed_aad_len=5,
-                                               status=status))
+        for _ in range(reps):
+            tlsgpu.seal_batch(c, tlsgpu.make_batch(n, inp, sealed, nonces, aad=aad, fixed_len=L,
+                                                   in_stride=L, out_stride=so, fixed_aad_len=5))
+            tlsgpu.open_batch(c, tlsgpu.make_batch(n, sealed, back, nonces, aad=aad, fixed_len=L,
+                                                   in_stride=so, out_stride=L, fixed_aad_len=5,
+                                                   status=status))
         torch.cuda.synchronize()
         # PROF_NOCHECK=1: measurement builds whose output is not the AEAD's
         assert os.environ.get("PROF_NOCHECK") == "1" or int(status.sum()) == n

@@ -2,7 +2,8 @@
 # HBM traffic of the headline kernels, per launch, calibrated per access shape:
 # separate rocprofv3 --pmc passes (FETCH_SIZE, WRITE_SIZE; no tracing) over
 # (1) tools/fetch_calib (4 GiB copies in each access shape the kernels use)
-# and (2) one launch of each kernel at bench.py's headline config; then
+# and (2) one launch of each kernel at bench.py's headline config and one
+# config-4 seal + open (bench.py --config c4); then
 # tools/traffic_summary.py derives each shape's factor and writes
 # <out>/traffic.json.   usage: tools/traffic.sh <outdir-under-gpurun_out>
 set -e
@@ -15,6 +16,8 @@ for c in FETCH_SIZE WRITE_SIZE; do
       -- $R/tools/fetch_calib > $OUT/cal_$c.log 2>&1
   timeout -k 10 300 rocprofv3 --pmc $c --output-format csv -d $OUT/bench_$c -o pass \
       -- python3 $R/bench.py --steps 1 --warmup 0 --no-cpu-baseline > $OUT/bench_$c.log 2>&1
+  timeout -k 10 300 rocprofv3 --pmc $c --output-format csv -d $OUT/bench_c4_$c -o pass \
+      -- python3 $R/bench.py --config c4 --steps 1 --warmup 0 --no-cpu-baseline > $OUT/bench_c4_$c.log 2>&1
 done
 python3 $R/tools/traffic_summary.py $OUT > $OUT/traffic.json
 cat $OUT/traffic.json
