@@ -73,10 +73,23 @@ __device__ __forceinline__ uint4 gmul_lowreg(uint4 y) {
 // of lane l come from a 16-row LDS table at ``jt`` (row l % 16: byte k of word
 // q = ((l + 4 q + k) % 16) * 16).  lane16 = l % 16.  At most eight table rows
 // in flight (32 VGPRs).
+// The word rotation by (l % 16) / 4 is two stages of per-lane selects (one
+// v_bitop3 each, VGPR operands: full rate); written as conditional swaps the
+// compiler emitted exec-masked v_mov chains, 15 moves and 4 exec updates per
+// multiply.
+__device__ __forceinline__ uint32_t sel32(uint32_t m, uint32_t t, uint32_t f) {   // m ? t : f, bitwise
+#if defined(__HIP_DEVICE_COMPILE__)
+    return __builtin_amdgcn_bitop3_b32(m, t, f, 0xca);
+#else
+    return (m & t) | (~m & f);
+#endif
+}
 __device__ __forceinline__ uint4 gmul_rot_j(uint4 y, uint32_t lane16, uint4 jw) {
-    uint32_t u0 = y.x, u1 = y.y, u2 = y.z, u3 = y.w;
-    if (lane16 & 8u) { uint32_t t = u0; u0 = u2; u2 = t; t = u1; u1 = u3; u3 = t; }
-    if (lane16 & 4u) { uint32_t t = u0; u0 = u1; u1 = u2; u2 = u3; u3 = t; }
+    const uint32_t m8 = 0u - ((lane16 >> 3) & 1u), m4 = 0u - ((lane16 >> 2) & 1u);
+    const uint32_t h0 = sel32(m8, y.z, y.x), h1 = sel32(m8, y.w, y.y);
+    const uint32_t h2 = sel32(m8, y.x, y.z), h3 = sel32(m8, y.y, y.w);
+    const uint32_t u0 = sel32(m4, h1, h0), u1 = sel32(m4, h2, h1);
+    const uint32_t u2 = sel32(m4, h3, h2), u3 = sel32(m4, h0, h3);
     const uint32_t s8 = (lane16 & 3u) << 3;
     const uint32_t v[4] = {__builtin_amdgcn_alignbit(u1, u0, s8), __builtin_amdgcn_alignbit(u2, u1, s8),
                            __builtin_amdgcn_alignbit(u3, u2, s8), __builtin_amdgcn_alignbit(u0, u3, s8)};
