@@ -195,6 +195,15 @@ def main():
         # ranks' exit status (rank 0 prints the JSON line)
         if args.config in ("c4", "ingest"):
             ap.error("--config %s runs on one GPU (BASELINE configs[3] / the host pipeline)" % args.config)
+        backend = os.environ.get("TLSGPU_DIST_BACKEND", "nccl")
+        if backend == "nccl":
+            import torch   # device_count() does not initialise the GPU
+            ndev = torch.cuda.device_count()
+            if ndev < args.gpus:
+                print("--gpus %d under nccl needs one GPU per rank, %d visible "
+                      "(TLSGPU_DIST_BACKEND=gloo rehearses the ranks on fewer)" % (args.gpus, ndev),
+                      file=sys.stderr)
+                sys.exit(2)
         import subprocess
         sys.stdout.flush()
         sys.exit(subprocess.call(rank_launch_cmd(sys.argv[1:], args.gpus, free_port())))
@@ -215,7 +224,11 @@ def main():
     from tlsgpu import distributed as tgd
     from vectors import tls13_aad
 
-    world, rank, local, device = tgd.init_process(torch, dist)
+    try:
+        world, rank, local, device = tgd.init_process(torch, dist)
+    except tgd.DistError as e:
+        print("rank setup: %s" % e, file=sys.stderr)
+        sys.exit(2)
     n, L = args.records, args.len
     first, _ = tgd.weak_shard(n, world, rank)   # this rank: seq [rank n, (rank + 1) n)
     # sealed records are ct||tag (the wire form), packed at a stride rounded up
@@ -519,7 +532,11 @@ def run_config5(args):
     import torch.distributed as dist
     import tlsgpu
     from tlsgpu import distributed as tgd
-    world, rank, _, _ = tgd.init_process(torch, dist)
+    try:
+        world, rank, _, _ = tgd.init_process(torch, dist)
+    except tgd.DistError as e:
+        print("rank setup: %s" % e, file=sys.stderr)
+        sys.exit(2)
     n, L = args.records, C5_APP
     first, _ = tgd.weak_shard(n, world, rank)
     DS, WS, H = c5_layout(L)

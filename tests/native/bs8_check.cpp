@@ -88,17 +88,25 @@ static int run(int klen, unsigned seed) {
         uint32_t lane[SB + 3], kmask;
         tg::bs8::lane_consts<SB>(c0, lane, kmask);
         for (uint32_t beta : betas) {
-            if ((uint64_t)beta << (SB + 3) >= (1ull << 31)) continue;   // counters stay 32-bit
+          if ((uint64_t)beta << (SB + 3) >= (1ull << 31)) continue;   // counters stay 32-bit
+          const bool hi = (beta + 1u) >> (16 - (SB + 3));
+          // pre01: rows 0-1 enter after round 1's SubBytes, computed once from
+          // the record planes (the kernels' path for counters below 2^16)
+          for (int pre01 = 0; pre01 <= (hi ? 0 : 1); ++pre01) {
             uint32_t s[4][8], w[4][8];
             for (int i = 0; i < 4; ++i)
                 for (int b = 0; b < 8; ++b) s[i][b] = tg::bs8::rec_plane(u, 8 * i + b);
+            if (pre01) {
+                tg::bs::sbox(s[0]);
+                tg::bs::sbox(s[1]);
+            }
             for (int b = 0; b < SB + 3; ++b) s[3 - (b >> 3)][b & 7] ^= lane[b];
             tg::bs8::ctr_planes<SB + 3, 16, SB + 3>(s, kmask, beta);
-            if ((beta + 1u) >> (16 - (SB + 3))) tg::bs8::ctr_planes<16, 32, SB + 3>(s, kmask, beta);
+            if (hi) tg::bs8::ctr_planes<16, 32, SB + 3>(s, kmask, beta);
             if (FOLD)
-                tg::bs8::encrypt<NR>(s, kf, w);
+                tg::bs8::encrypt<NR>(s, kf, w, !pre01);
             else
-                tg::bs8::encrypt<NR>(s, km, w);
+                tg::bs8::encrypt<NR>(s, km, w, !pre01);
             for (int j = 0; j < 8; ++j) {
                 const uint32_t ctr = c0 + (beta << (SB + 3)) + ((uint32_t)j << SB);
                 uint8_t blk[16], want[16];
@@ -117,6 +125,7 @@ static int run(int klen, unsigned seed) {
                 }
                 ++checked;
             }
+          }
         }
     }
     printf("NR=%d fold=%d lanes=%u seed=%u blocks=%d bad=%d\n", NR, (int)FOLD, L, seed, checked, bad);

@@ -59,6 +59,14 @@ def test_world_mismatch_refused():
     assert "--gpus 2 but WORLD_SIZE=1" in r.stderr
 
 
+def test_nccl_needs_a_gpu_per_rank():
+    """Under nccl (the default backend) --gpus N with fewer visible devices
+    is refused before any rank starts."""
+    r = _run(["--gpus", "2", "--records", "64", "--no-cpu-baseline"], {"TLSGPU_DIST_BACKEND": "nccl"})
+    assert r.returncode == 2, r.stderr[-2000:]
+    assert "needs one GPU per rank, 0 visible" in r.stderr
+
+
 @pytest.mark.parametrize("config", ["c4", "ingest"])
 def test_single_gpu_configs_refuse_n(config):
     r = _run(["--gpus", "2", "--config", config])

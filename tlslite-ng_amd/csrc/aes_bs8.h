@@ -310,12 +310,34 @@ TG_BS_HD void to_blocks(uint32_t (*x)[8], uint32_t (*w)[8]) {
 // Rounds 1..NR on the state after AddRoundKey 0 (in place); w receives the
 // blocks (to_blocks).  Middle rounds are a rolled loop on the device (a
 // round is ~500 instructions).
+//
+// sub01 = false: rows 0 and 1 of s already hold round 1's SubBytes output.
+// In counter mode with counters below 2^16 those rows are the nonce bytes and
+// counter bytes 12-13 (zero), the same for every block of a record, so the
+// caller computes their S-box once per record (rows 2 and 3 carry counter
+// bytes 14 and 15): two of the four S-box calls of round 1 (144 of ~4 500
+// instructions per batch of eight blocks).
 template <int NR, class KM>
-TG_BS_HD void encrypt(uint32_t (*s)[8], const KM& km, uint32_t (*w)[8]) {
+TG_BS_HD void encrypt(uint32_t (*s)[8], const KM& km, uint32_t (*w)[8], bool sub01 = true) {
+    // round 1 peeled off the rolled loop: its S-box of rows 0-1 is optional
+    if (sub01) {
+        bs::sbox(s[0]);
+        TG_BS8_FENCE();
+        bs::sbox(s[1]);
+        TG_BS8_FENCE();
+    }
+    bs::sbox(s[2]);
+    TG_BS8_FENCE();
+    bs::sbox(s[3]);
+    TG_BS8_FENCE();
+    if constexpr (KM::kFolded)
+        mix_round_folded(s, km, 1);
+    else
+        mix_round(s, km, 1);
 #if defined(__HIP_DEVICE_COMPILE__)
 #pragma unroll 1
 #endif
-    for (int r = 1; r < NR; ++r) {
+    for (int r = 2; r < NR; ++r) {
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
             bs::sbox(s[i]);

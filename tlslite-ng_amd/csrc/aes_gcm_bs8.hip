@@ -36,14 +36,19 @@
 namespace tg {
 namespace {
 
+// Per-wave LDS of octet_job: the first-state planes of each record (128 B per
+// record slot, up to 8) at recw, and round 1's S-box output of their rows 0
+// and 1 (64 B per slot) at recw + 1024.
+constexpr uint32_t kRecArea = 1536;
+
 constexpr int kBs8Threads = 512;
 constexpr int kBs8Recs = kBs8Threads / 8;               // record slots per workgroup
 constexpr uint32_t kTeBase = 65536;                       // hybrid kernel: Te0/Te2 copies
 constexpr uint32_t kBs8Sbox = 65536;                      // 256-byte S-box
 constexpr uint32_t kBs8Jt = 65536 + 256;                  // gmul_rot lane-offset rows (256 B)
 constexpr uint32_t kBs8Keys = kBs8Jt + 256;               // round-key planes (bs8::KeyPlanesLds)
-constexpr uint32_t kBs8RecBase = kBs8Keys + 2048;          // 128 B of planes per record slot
-constexpr size_t kBs8Lds = kBs8RecBase + (kBs8Threads / 64) * 1024;
+constexpr uint32_t kBs8RecBase = kBs8Keys + 2048;          // kRecArea per wave (octet_job)
+constexpr size_t kBs8Lds = kBs8RecBase + (kBs8Threads / 64) * kRecArea;
 
 // No static __shared__ in this file: the GHASH tables sit at LDS address 0
 // (gmul's absolute addresses).
@@ -191,6 +196,7 @@ __device__ __forceinline__ void octet_job(const KC& kc, const tg_batch& b,
     const uint32_t nfull = len >> 4, tail = len & 15, nc = (len + 15) >> 4, na = (alen + 15) >> 4;
     const uint32_t rho = (l + nc + 1u) & kM;   // this lane's ciphertext blocks: rho + LPR v
     const uint32_t recb = recw + (lane >> kS) * 128u;
+    const uint32_t rsub = recw + 1024u + (lane >> kS) * 64u;   // rows 0-1 after round 1's SubBytes
     const uint32_t lane4 = ((lane & 31u) << 2) | kTeBase;
     CtrCache cc = {0, 0, 0, 0};
     if (TROLE) {
@@ -201,6 +207,17 @@ __device__ __forceinline__ void octet_job(const KC& kc, const tg_batch& b,
         const uint4 rp = make_uint4(bs8::rec_plane(u, e), bs8::rec_plane(u, e + 1),
                                     bs8::rec_plane(u, e + 2), bs8::rec_plane(u, e + 3));
         if (l < 8) lds_st128(recb + 16u * l, rp);   // read back by the same wave (in order per wave)
+        __builtin_amdgcn_wave_barrier();
+        // rows 0 and 1 hold no counter byte below 2^16 (bs8::encrypt, sub01):
+        // their round-1 SubBytes once per record, lane l % 2 doing row l % 2
+        uint32_t r[8];
+        const uint4 a = lds_u128(recb + 32u * (l & 1u)), c = lds_u128(recb + 32u * (l & 1u) + 16u);
+        r[0] = a.x; r[1] = a.y; r[2] = a.z; r[3] = a.w; r[4] = c.x; r[5] = c.y; r[6] = c.z; r[7] = c.w;
+        bs::sbox(r);
+        if (l < 2) {
+            lds_st128(rsub + 32u * l, make_uint4(r[0], r[1], r[2], r[3]));
+            lds_st128(rsub + 32u * l + 16u, make_uint4(r[4], r[5], r[6], r[7]));
+        }
         __builtin_amdgcn_wave_barrier();
     }
     const bool aligned = (((uintptr_t)in | (uintptr_t)out) & 15) == 0;
@@ -304,10 +321,13 @@ __device__ __forceinline__ void octet_job(const KC& kc, const tg_batch& b,
             uint4 ks[1] = {xor4(aes_block_sb<NR>(rk, make_uint4(nvr.x, nvr.y, nvr.z, bswap32(c0)), sbox), rkl)};
             consume(ks, blk0, 0, std::integral_constant<int, 1>(), nullptr);
         } else {
+            // counters of this batch below 2^16 (wave-uniform): rows 0-1
+            // come in after round 1's SubBytes (bs8::encrypt sub01)
+            const bool hi = (beta + 1u) >> (16 - (kS + 3));
             uint32_t s[4][8];
 #pragma unroll
             for (int q = 0; q < 8; ++q) {
-                const uint4 v = lds_u128(recb + 16u * q);
+                const uint4 v = lds_u128((q < 4 && !hi ? rsub : recb) + 16u * q);
                 s[q >> 1][4 * (q & 1) + 0] = v.x;
                 s[q >> 1][4 * (q & 1) + 1] = v.y;
                 s[q >> 1][4 * (q & 1) + 2] = v.z;
@@ -318,7 +338,7 @@ __device__ __forceinline__ void octet_job(const KC& kc, const tg_batch& b,
 #pragma unroll
             for (int bb = 0; bb < (int)kS + 3; ++bb) s[3 - (bb >> 3)][bb & 7] ^= lanec[bb];
             bs8::ctr_planes<kS + 3, 16, kS + 3>(s, kmask, beta);
-            if ((beta + 1u) >> (16 - (kS + 3))) bs8::ctr_planes<16, 32, kS + 3>(s, kmask, beta);
+            if (hi) bs8::ctr_planes<16, 32, kS + 3>(s, kmask, beta);
             // PRE: the batch's payload is loaded before the cipher runs, so
             // the XOR does not wait for HBM (32 VGPRs live across encrypt():
             // only at three waves per SIMD; at four the seal kernel spilled
@@ -330,7 +350,7 @@ __device__ __forceinline__ void octet_job(const KC& kc, const tg_batch& b,
                 for (int q = 0; q < 8; ++q) dp[q] = gload16u(in + 16u * (blk0 + LPR * q));
             }
             uint32_t w[4][8];
-            bs8::encrypt<NR>(s, km, w);
+            bs8::encrypt<NR>(s, km, w, hi);
             uint4 ks[8];
 #pragma unroll
             for (int j = 0; j < 8; ++j) ks[j] = make_uint4(w[0][j], w[1][j], w[2][j], w[3][j]);
@@ -395,7 +415,7 @@ __global__ __launch_bounds__(kBs8Threads, 4) void gcm_bs8_kernel(const GcmKeyDev
     const uint32_t wave = threadIdx.x >> 6;
     octet_job<NR, OPEN, false>(SingleKeyCtx{key, kBs8Jt}, b, order,
                                (uint64_t)blockIdx.x * kBs8Recs + 8u * wave,
-                               kBs8RecBase + wave * 1024u, RkLds{0}, kBs8Sbox,
+                               kBs8RecBase + wave * kRecArea, RkLds{0}, kBs8Sbox,
                                bs8::KeyPlanesLds{kBs8Keys});
 }
 
@@ -416,7 +436,7 @@ constexpr uint32_t kHyRk = kHySbox + 256;               // 15 round keys (16 B e
 constexpr uint32_t kHyJt = kHyRk + 256;                 // gmul_rot lane-offset rows
 constexpr uint32_t kHyKeys = kHyJt + 256;               // round-key planes (bs8::KeyPlanesLds)
 constexpr uint32_t kHyRecBase = kHyKeys + 2048;
-constexpr size_t kHyLds = kHyRecBase + (kHyThreads / 64) * 1024;   // for either size
+constexpr size_t kHyLds = kHyRecBase + (kHyThreads / 64) * kRecArea;   // for either size
 static_assert(kTeBase == 65536, "Te block follows the GHASH tables");
 
 // The batch descriptor is read from memory per job (bp): held in SGPRs
@@ -440,7 +460,7 @@ __global__ __launch_bounds__(THREADS) void gcm_hy_kernel(const GcmKeyDev* __rest
     __syncthreads();
     const uint32_t wave = (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
     const uint64_t njobs = (bp->n + 7) / 8;
-    const uint32_t recw = kHyRecBase + wave * 1024u;
+    const uint32_t recw = kHyRecBase + wave * kRecArea;
     const uint4 jw = lds_u128(kHyJt + ((threadIdx.x & 15u) << 4));
     if (wave < nt) {
         if (prio) __builtin_amdgcn_s_setprio(1);
@@ -555,8 +575,8 @@ int launch_hy(const GcmKeyDev* key, const tg_batch& b, hipStream_t s, const uint
 constexpr int kKtThreads = 256;
 constexpr int kKtWaves = kKtThreads / 64;
 constexpr uint32_t kKtSbox = kKtWaves * 8192;            // after the per-wave tables
-constexpr uint32_t kKtRecBase = kKtSbox + 256;           // 1 KiB of record planes per wave
-constexpr size_t kKtLds = kKtRecBase + kKtWaves * 1024;
+constexpr uint32_t kKtRecBase = kKtSbox + 256;           // kRecArea per wave (octet_job)
+constexpr size_t kKtLds = kKtRecBase + kKtWaves * kRecArea;
 constexpr int kKtPlaneWords = 15 * 32;                   // per key in the plane table
 
 template <int NR, bool OPEN, int LPR>
@@ -580,7 +600,7 @@ __global__ __launch_bounds__(kKtThreads, 4) void gcm_kt_kernel(const GcmTableKey
     // to the lane kernel: short ones and out-of-range key indices
     if (p0 >= *nlong_p) return;
     const uint32_t k = (uint32_t)__builtin_amdgcn_readfirstlane((int)gld(b.key_idx, gld(order, p0)));
-    const uint32_t tab = 8192u * wave, recw = kKtRecBase + wave * 1024u;
+    const uint32_t tab = 8192u * wave, recw = kKtRecBase + wave * kRecArea;
     build_table4(tab, hpow[64u * k + LPR - 1u]);   // this wave's GHASH tables: the key's H^LPR
     __builtin_amdgcn_wave_barrier();
     b.n = p1;   // the job's slots are p0 .. p1 - 1 (at most 64 / LPR)
