@@ -105,7 +105,12 @@ __device__ __forceinline__ void t_half(uint32_t lane4, const RkLds& rk, const Ct
             s[q][3] = col(a3, a0, a1, a2, k.w, lane4);
         }
     }
+    // rolled (TG_T_UNROLL: the measurement build with the rounds unrolled)
+#if defined(TG_T_UNROLL)
 #pragma unroll
+#else
+#pragma unroll 1
+#endif
     for (int r = 3; r < NR; ++r) {
         const uint4 k = rk.get(r);
 #pragma unroll
@@ -298,7 +303,11 @@ __device__ __forceinline__ void octet_job(const KC& kc, const tg_batch& b,
             const bool win = __all(((c0 ^ (c0 + 56u)) >> 8) == 0);
             const uint32_t k0w = rkT.get(0).w;
             const uint4 wc = win ? win_consts<NR>(lane4, rkT, cc, c0) : make_uint4(0, 0, 0, 0);
+#if defined(TG_T_UNROLL)
 #pragma unroll
+#else
+#pragma unroll 1
+#endif
             for (int h = 0; h < 2; ++h) {
                 if (h == 1 && __all(!valid || nvl <= 8u * beta + 4u)) break;
                 uint4 ks[4];
