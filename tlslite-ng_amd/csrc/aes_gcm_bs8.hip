@@ -105,11 +105,16 @@ __device__ __forceinline__ void t_half(uint32_t lane4, const RkLds& rk, const Ct
             s[q][3] = col(a3, a0, a1, a2, k.w, lane4);
         }
     }
-    // rolled (TG_T_UNROLL: the measurement build with the rounds unrolled)
+    // two rounds per iteration: fully unrolled, the T-table code did not fit
+    // the instruction cache beside the bitsliced role's; one
+    // round per iteration measured 1.3 % slower than two (measurement builds:
+    // TG_T_UNROLL, TG_T_UNROLL1)
 #if defined(TG_T_UNROLL)
 #pragma unroll
-#else
+#elif defined(TG_T_UNROLL1)
 #pragma unroll 1
+#else
+#pragma unroll 2
 #endif
     for (int r = 3; r < NR; ++r) {
         const uint4 k = rk.get(r);
