@@ -618,18 +618,24 @@ __global__ __launch_bounds__(kKtThreads, 4) void gcm_kt_kernel(const GcmTableKey
     build_table4(tab, hpow[64u * k + LPR - 1u]);   // this wave's GHASH tables: the key's H^LPR
     __builtin_amdgcn_wave_barrier();
     b.n = p1;   // the job's slots are p0 .. p1 - 1 (at most 64 / LPR)
-    octet_job<NR, OPEN, false, bs8::KeyPlanes, TableKeyCtx, false, LPR>(
+    octet_job<NR, OPEN, false, bs8::KeyPlanesVmemFolded, TableKeyCtx, false, LPR>(
         TableKeyCtx{keys[k].rk, hpow + 64u * k, tab}, b, order, p0, recw, RkLds{0}, kKtSbox,
-        bs8::KeyPlanes{planes + kKtPlaneWords * k});
+        bs8::KeyPlanesVmemFolded{{reinterpret_cast<const uint4*>(planes + kKtPlaneWords * k)}});
 }
 
+// Per key, the hybrid kernel's key rows (hy_setup_kernel): the
+// MixColumns-folded planes (keymath.h bs8_fold_word) of rounds 1 .. nr - 1 and
+// the round-key planes of rounds 0 and nr, row (8 r + bit) = the four rows' words.
 __global__ void kt_planes_kernel(const GcmTableKey* __restrict__ keys, uint64_t n, int nr,
                                  uint32_t* __restrict__ planes) {
     const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const uint64_t k = t / kKtPlaneWords;
     const int e = (int)(t % kKtPlaneWords);
     if (k >= n) return;
-    planes[t] = e < 32 * (nr + 1) ? bs8_mask_word(keys[k].rk, e) : 0u;
+    const int r = e >> 5, i = (e >> 3) & 3, bit = e & 7;
+    const uint32_t w = e >= 32 * (nr + 1) ? 0u
+                       : r >= 1 && r < nr ? bs8_fold_word(keys[k].rk, e) : bs8_mask_word(keys[k].rk, e);
+    planes[k * kKtPlaneWords + 4 * (8 * r + bit) + i] = w;
 }
 
 // Key-table AES-GCM by record length (BASELINE config 4): records of at

@@ -154,7 +154,8 @@ bool is_ccm(int alg) { return alg == TG_AES_CCM || alg == TG_AES_CCM_8; }
 
 // A multi-key AES-GCM allocation: GcmTableKey[nkeys], then the 64 GHASH
 // powers of each key (gcm_table_wave_kernel, gcm_kt_kernel), then the 15 x 32
-// bitsliced round-key planes of each key (gcm_kt_kernel).
+// bitsliced key-plane words of each key, MixColumns-folded, in the hybrid
+// kernel's row layout (gcm_kt_kernel, kt_planes_kernel).
 constexpr size_t kTableHpowBytes = 64 * sizeof(uint4);
 constexpr size_t kTablePlaneBytes = 15 * 32 * sizeof(uint32_t);
 uint4* table_hpow(const tg_key* k) {

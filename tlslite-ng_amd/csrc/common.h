@@ -276,7 +276,7 @@ int tg_key_job_plan(const uint32_t* key_idx, const uint32_t* len, uint32_t fixed
                     uint32_t* njobs, uint32_t* nlong, void* scratch, size_t* bytes, hipStream_t s);
 // Key-table AES-GCM (aes_gcm_bs8.hip launch_kt): records of at least
 // ``split`` bytes through the key-grouped octet kernel (planes = per-key
-// bitsliced round-key planes, tg_launch_kt_planes; hpow = the keys'
+// bitsliced key rows, MixColumns-folded, tg_launch_kt_planes; hpow = the keys'
 // H^1..H^64), the others through the lane kernel.
 // lpr: lanes per record of the key-grouped bitsliced kernel for the long
 // records (8, 16, 32 or 64), or 0 for the wave-per-record T-table kernel
