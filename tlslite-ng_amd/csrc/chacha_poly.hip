@@ -272,9 +272,16 @@ __device__ __forceinline__ void tiled_blocks_dma(WaveTile& t, uint32_t lane,
             const uint32_t r = 32 * g + 8 * q + rq;
             const uint32_t c = swz(r, cq);          // the chunk that lands in slot cq
             const uint32_t off = p0 + (c >> 2) < jmin ? 64 * p0 + 16 * c : 16 * (c & 3u);
-            const uint8_t* src = reinterpret_cast<const uint8_t*>(((uint64_t)P[q].y << 32) | P[q].x);
+#if defined(TG_CHACHA_ILV)   // measurement build: the group's lines interleaved (wrong bytes, same volume)
+            const uint4 b0 = t.ptr[32 * g];
+            const uint8_t* src = reinterpret_cast<const uint8_t*>(((uint64_t)b0.y << 32) | b0.x) +
+                                 ((p0 >> 1) * 32u + 8u * q + rq) * 128u + 16u * c;
+            (void)off;
+#else
+            const uint8_t* src = reinterpret_cast<const uint8_t*>(((uint64_t)P[q].y << 32) | P[q].x) + off;
+#endif
             __builtin_amdgcn_global_load_lds(
-                (const __attribute__((address_space(1))) void*)(src + off),
+                (const __attribute__((address_space(1))) void*)src,
                 (__attribute__((address_space(3))) void*)(&t.row[32 * g + 8 * q][0]),
                 16, 0, 0);
         }
@@ -295,8 +302,14 @@ __device__ __forceinline__ void tiled_blocks_dma(WaveTile& t, uint32_t lane,
         const uint32_t blk = p0 + (cq >> 2);
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
+#if defined(TG_CHACHA_ILV)
+            const uint4 b0 = t.ptr[32 * g];
+            uint8_t* dst = reinterpret_cast<uint8_t*>(((uint64_t)b0.w << 32) | b0.z);
+            if (blk < jmin && dst) gstore16(dst + ((p0 >> 1) * 32u + 8u * q + rq) * 128u + 16u * cq, S[q]);
+#else
             uint8_t* dst = reinterpret_cast<uint8_t*>(((uint64_t)P[q].w << 32) | P[q].z);
             if (blk < jmin && dst) gstore16(dst + 64 * p0 + 16 * cq, S[q]);
+#endif
         }
         if (p0 + 2 < jmin) fetch_pair(g, p0 + 2, P);
     };
