@@ -162,7 +162,11 @@ struct TableKeyCtx {    // a key of a key table: the wave's 4-bit H^8 tables in 
     uint32_t tab;
     __device__ __forceinline__ const uint32_t* rk() const { return rkw; }
     __device__ __forceinline__ uint4 hpow(int e) const { return hp[e - 1]; }
+#if defined(TG_KT_NO_GHASH)   // measurement build: no GHASH multiply (wrong tags)
+    __device__ __forceinline__ uint4 gmul(uint4 y) const { return y; }
+#else
     __device__ __forceinline__ uint4 gmul(uint4 y) const { return gmul4(y, tab); }
+#endif
 };
 
 // One octet job: the eight records of record slots t0 .. t0 + 7 on this wave
@@ -615,7 +619,9 @@ __global__ __launch_bounds__(kKtThreads, 4) void gcm_kt_kernel(const GcmTableKey
     if (p0 >= *nlong_p) return;
     const uint32_t k = (uint32_t)__builtin_amdgcn_readfirstlane((int)gld(b.key_idx, gld(order, p0)));
     const uint32_t tab = 8192u * wave, recw = kKtRecBase + wave * kRecArea;
+#if !defined(TG_KT_NO_BUILD)   // measurement build: tables left as they are (wrong tags)
     build_table4(tab, hpow[64u * k + LPR - 1u]);   // this wave's GHASH tables: the key's H^LPR
+#endif
     __builtin_amdgcn_wave_barrier();
     b.n = p1;   // the job's slots are p0 .. p1 - 1 (at most 64 / LPR)
     octet_job<NR, OPEN, false, bs8::KeyPlanesVmemFolded, TableKeyCtx, false, LPR>(
