@@ -265,18 +265,27 @@ __device__ __forceinline__ void build_table4(uint32_t tab, uint4 gn) {
 __device__ __forceinline__ uint4 gmul4(uint4 y, uint32_t tab) {
     const uint32_t w[4] = {y.x, y.y, y.z, y.w};
     uint4 z = make_uint4(0, 0, 0, 0);
+    // the nibble mask in a VGPR: (x & m) | tab is then one full-rate
+    // v_bitop3 (an SGPR or literal operand makes it half rate or two ops)
+    uint32_t m = 0xf0u;
+#if defined(__HIP_DEVICE_COMPILE__)
+    asm volatile("v_mov_b32 %0, 0xf0" : "=v"(m));
+#endif
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
         uint4 e[8];
+        uint32_t w4 = w[q] << 4;   // opaque: or (w4 >> 8k) & m becomes a half-rate v_bfe_u32
+#if defined(__HIP_DEVICE_COMPILE__)
+        asm volatile("" : "+v"(w4));
+#endif
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
             const uint32_t B = 4 * q + k;
-            const uint32_t hi = k ? (w[q] >> (8 * k)) & 0xf0u : w[q] & 0xf0u;
-            const uint32_t lo = k ? (w[q] >> (8 * k - 4)) & 0xf0u : (w[q] << 4) & 0xf0u;
-            // (nibble | tab) + constant: the constant rides in the ds_read
-            // offset field and nothing table-shaped is loop-invariant
-            e[2 * k] = lds_u128((hi | tab) + 512u * B);
-            e[2 * k + 1] = lds_u128((lo | tab) + 512u * B + 256u);
+            const uint32_t hi = ((w[q] >> (8 * k)) & m) | tab;
+            const uint32_t lo = ((w4 >> (8 * k)) & m) | tab;
+            // nibble | tab, plus a constant that rides in the ds_read offset field
+            e[2 * k] = lds_u128(hi + 512u * B);
+            e[2 * k + 1] = lds_u128(lo + 512u * B + 256u);
         }
         z = xor4_3(z, e[0], e[1]);
         z = xor4_3(z, e[2], e[3]);
