@@ -77,8 +77,8 @@ int tg_init(int device);                   /* hipSetDevice for the calling threa
  *   waves_per_record   0 auto, 1 / 4 / 16
  *   no_plan            1 = no length-sorted launch order
  *   stage_copy         1 = per-record calls copy through device memory
- *   hy_t, hy_noprio    hybrid AES-GCM kernel: T-table waves (0 = half,
- *                      -1 = none), 1 = T-table waves at normal priority
+ *   hy_t, hy_prio      hybrid AES-GCM kernel: T-table waves (0 = auto: 10
+ *                      of 16, -1 = none), 1 = T-table waves at raised priority
  *   hy_threads         hybrid AES-GCM workgroup: 0 = 1024, or 768
  * An unknown name is TG_EINVAL; a variant a launcher does not know makes
  * its launches fail with TG_EINVAL. */

@@ -36,6 +36,9 @@ LENS = [0, 1, 15, 16, 17, 63, 64, 65, 1000, 1024, 1040, 4095, 16383, 16384, 1638
     ("aesgcm", 32, {"gcm_variant": 15}),
     ("aesgcm", 16, {"gcm_variant": 15, "hy_threads": 768}),   # 3 waves / SIMD, payload prefetch
     ("aesgcm", 32, {"gcm_variant": 15, "hy_threads": 768}),
+    ("aesgcm", 16, {"gcm_variant": 15, "hy_t": 8, "hy_prio": 1}),   # round 2's split
+    ("aesgcm", 16, {"gcm_variant": 15, "hy_t": 16}),   # T-table waves only
+    ("aesgcm", 32, {"gcm_variant": 15, "hy_t": -1}),   # bitsliced waves only
     ("chacha", 32, {"chacha_variant": 4}),        # lane per record, register-staged tile fill
     ("chacha", 32, {"chacha_variant": 5}),        # lane per record, LDS-DMA tile fill (auto)
     ("chacha", 32, {"chacha_variant": 3}),        # wave per record

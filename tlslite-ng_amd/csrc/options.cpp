@@ -23,7 +23,7 @@ constexpr OptName kNames[kOptCount] = {
     {"no_plan", "TLSGPU_NO_PLAN"},
     {"stage_copy", "TLSGPU_STAGE_COPY"},
     {"hy_t", "TLSGPU_HY_T"},
-    {"hy_noprio", "TLSGPU_HY_NOPRIO"},
+    {"hy_prio", "TLSGPU_HY_PRIO"},
     {"kt_split", "TLSGPU_KT_SPLIT"},
     {"kt_lpr", "TLSGPU_KT_LPR"},
     {"hy_threads", "TLSGPU_HY_THREADS"},

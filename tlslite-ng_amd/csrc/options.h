@@ -17,8 +17,8 @@ enum Opt {
     kOptWavesPerRecord,       // TLSGPU_WAVES_PER_RECORD: 1 / 4 / 16, 0 = by batch size
     kOptNoPlan,               // TLSGPU_NO_PLAN: 1 = no length-sorted launch order
     kOptStageCopy,            // TLSGPU_STAGE_COPY: 1 = per-record calls copy through HBM
-    kOptHyT,                  // TLSGPU_HY_T: T-table waves of the hybrid kernel (0 = 8)
-    kOptHyNoPrio,             // TLSGPU_HY_NOPRIO: 1 = T-table waves at normal priority
+    kOptHyT,                  // TLSGPU_HY_T: T-table waves of the hybrid kernel (0 = 10 of 16)
+    kOptHyPrio,               // TLSGPU_HY_PRIO: 1 = T-table waves at raised priority
     kOptKtSplit,              // TLSGPU_KT_SPLIT: key-table length split in bytes, 0 = auto
     kOptKtLpr,                // TLSGPU_KT_LPR: key-table long records, lanes per record
                               // (8 / 16 / 32 / 64), -1 wave-per-record T-table, 0 auto

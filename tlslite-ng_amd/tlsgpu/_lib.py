@@ -157,7 +157,7 @@ def check(rc):
 def set_option(name, value):
     """Set a process-wide kernel-selection option (include/tlsgpu.h
     tg_set_option: gcm_variant, gcm_table_variant, kt_split, chacha_variant,
-    ccm_variant, waves_per_record, no_plan, stage_copy, hy_t, hy_noprio)."""
+    ccm_variant, waves_per_record, no_plan, stage_copy, hy_t, hy_prio)."""
     check(load().tg_set_option(name.encode(), int(value)))
 
 
