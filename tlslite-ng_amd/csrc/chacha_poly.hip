@@ -21,7 +21,10 @@
 namespace tg {
 namespace {
 
-constexpr int kChachaThreads = 256;
+#if !defined(TG_CHACHA_THREADS)   // measurement builds may override the workgroup size
+#define TG_CHACHA_THREADS 256
+#endif
+constexpr int kChachaThreads = TG_CHACHA_THREADS;
 
 #define QR(a, b, c, d)                                  \
     a += b; d ^= a; d = rotl32(d, 16);                  \
