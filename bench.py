@@ -410,6 +410,24 @@ def c4_traffic(path, op):
             "source": os.path.relpath(path, ROOT)}
 
 
+def c5_traffic(path, n, L_app):
+    """Config 5's HBM bytes per record seal of the whole batch (the framing
+    kernel and the AEAD kernel together) from the tools/traffic.sh summary,
+    or None (only for the default 2^20 x 16 KiB shape)."""
+    if n != 1 << 20 or L_app != C5_APP or not os.path.exists(path):
+        return None
+    with open(path) as f:
+        ks = json.load(f).get("kernels", {})
+    parts = [ks.get("c5_prep"), ks.get("c5_seal")]
+    if not all(parts):
+        return None
+    hbm = sum(k["hbm_bytes"] for k in parts)
+    return {"hbm_bytes": round(hbm),
+            "kernels": {"seal_prep": round(parts[0]["hbm_bytes"]), "gcm_hy_kernel": round(parts[1]["hbm_bytes"])},
+            "traffic_over_algorithmic": round(hbm / c5_algorithmic_bytes(n, L_app, "seal"), 3),
+            "source": os.path.relpath(path, ROOT)}
+
+
 def c5_algorithmic_bytes(n, L_app, op):
     """Config 5's record seal through the framing path (recordlayer.py:
     606-617 then 536-565): reads the L application bytes, writes the 5-byte
@@ -609,6 +627,10 @@ def run_config5(args):
                          "ms": round(ms, 3)},
             "oracle_checked_records": len(samples), "oracle_mismatches": bad,
             "verified": bool(ok)}
+        tr = c5_traffic(args.traffic_file, n, L) if world == 1 else None
+        if tr:
+            line["roofline"]["traffic"] = tr["hbm_bytes"]
+            line["roofline"]["traffic_detail"] = tr
         if not args.no_cpu_baseline and world == 1:
             cores = args.cpu_cores or host_cores()[0]
             line["cpu_baseline"] = cpu_baseline_c5(L, cores, args.cpu_seconds)

@@ -18,6 +18,10 @@ factors of its shape:
   c4_kt_*             gcm_kt_kernel (config 4's long records), octet layout
   c4_lane_*           gcm_table_vkernel (config 4's short records), 16 B per
                       lane, one record per lane -> the lane factors
+  c5_prep, c5_seal    config 5 (bench.py --config c5, collected from its own
+                      passes): seal_prep (one thread per record: header,
+                      inner type, nonce / AAD rows -> the lane factors) and
+                      the hybrid seal over the framed records (octet)
 
 Config 4 (bench.py --config c4) is one seal and one open of the whole batch;
 its traffic per operation is the sum over the kernels of that operation.
@@ -46,6 +50,8 @@ KERNELS = [(r"gcm_hy_kernel<10, false", "aes128gcm_seal", "octet", "octet"),
            (r"gcm_kt_kernel<14, true", "c4_kt_open", "octet", "octet"),
            (r"gcm_table_vkernel<14, false", "c4_lane_seal", "lane", "lane"),
            (r"gcm_table_vkernel<14, true", "c4_lane_open", "lane", "lane")]
+KERNELS_C5 = [(r"seal_prep", "c5_prep", "lane", "lane"),
+              (r"gcm_hy_kernel<10, false", "c5_seal", "octet", "octet")]
 
 
 def collect(d, pattern):
@@ -70,10 +76,10 @@ def main(d):
                 factors[shape] = {"fetch_size_bytes": fetch, "write_size_bytes": write,
                                   "fetch_factor": round(CAL_BYTES / fetch, 4) if fetch else None,
                                   "write_factor": round(CAL_BYTES / write, 4) if write else None}
-    raw = collect(d, "bench_*")
     out = {}
-    for name, c in raw.items():
-        for pat, lab, shape, cal in KERNELS:
+    for name, c, kernels in ([(n, c, KERNELS) for n, c in collect(d, "bench_*").items()] +
+                             [(n, c, KERNELS_C5) for n, c in collect(d, "c5_*").items()]):
+        for pat, lab, shape, cal in kernels:
             if re.search(pat, name) and cal in factors:
                 fetch, write = mean_kb(c["FETCH_SIZE"]), mean_kb(c["WRITE_SIZE"])
                 ff, wf = factors[cal]["fetch_factor"], factors[cal]["write_factor"]
