@@ -24,6 +24,9 @@ namespace {
 #if !defined(TG_CHACHA_THREADS)   // measurement builds may override the workgroup size
 #define TG_CHACHA_THREADS 256
 #endif
+#if !defined(TG_CHACHA_MINW)      // ... and the waves per SIMD of the lane kernel (VGPR budget)
+#define TG_CHACHA_MINW 4
+#endif
 constexpr int kChachaThreads = TG_CHACHA_THREADS;
 
 #define QR(a, b, c, d)                                  \
@@ -593,10 +596,10 @@ int launch_w(const ChachaKeyDev* keys, uint64_t nkeys, const tg_batch& b, hipStr
     const uint64_t blocks = (b.n + kChachaThreads - 1) / kChachaThreads;
     if (blocks > 0x7fffffffull) return TG_EINVAL;
     if (opt(kOptChachaVariant) == 4)   // register-staged tile fill
-        hipLaunchKernelGGL((chacha_kernel<OPEN, MULTIKEY, 4, false>), dim3((unsigned)blocks), dim3(kChachaThreads),
+        hipLaunchKernelGGL((chacha_kernel<OPEN, MULTIKEY, TG_CHACHA_MINW, false>), dim3((unsigned)blocks), dim3(kChachaThreads),
                            0, s, keys, nkeys, b, order);
     else                                // LDS-DMA tile fill
-        hipLaunchKernelGGL((chacha_kernel<OPEN, MULTIKEY, 4, true>), dim3((unsigned)blocks), dim3(kChachaThreads),
+        hipLaunchKernelGGL((chacha_kernel<OPEN, MULTIKEY, TG_CHACHA_MINW, true>), dim3((unsigned)blocks), dim3(kChachaThreads),
                            0, s, keys, nkeys, b, order);
     return hipGetLastError() == hipSuccess ? TG_OK : TG_EHIP;
 }
