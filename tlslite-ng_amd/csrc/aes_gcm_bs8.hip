@@ -78,6 +78,11 @@ __device__ __forceinline__ uint32_t wave_min_u32(uint32_t v) {
 // a window in this batch (a wave-uniform test), else full rounds.  Round keys
 // are read from LDS (wave-uniform address: one broadcast ds_read_b128 per
 // round), which keeps the 44 / 60 key words out of the SGPR file.
+// The hybrid kernel keeps its round keys rotated right by 8 bits kRkRot bytes
+// past the plain ones (RkLds base): the T-table columns of rounds 2 .. NR - 1
+// take them inside the rotation (aes_round.h col_r, one XOR per column fewer).
+constexpr uint32_t kRkRot = 512;
+
 template <int NR>
 __device__ __forceinline__ void t_half(uint32_t lane4, const RkLds& rk, const CtrCache& cc,
                                        uint32_t c0, bool win, const uint4& wc, uint32_t k0w, int h,
@@ -98,11 +103,11 @@ __device__ __forceinline__ void t_half(uint32_t lane4, const RkLds& rk, const Ct
             const uint32_t a1 = cc.k1 ^ T2<2>(s3, lane4);
             const uint32_t a2 = cc.k2 ^ rotl32(T0<1>(s3, lane4), 8);
             const uint32_t a3 = cc.k3 ^ T0<0>(s3, lane4);
-            const uint4 k = rk.get(2);
-            s[q][0] = col(a0, a1, a2, a3, k.x, lane4);
-            s[q][1] = col(a1, a2, a3, a0, k.y, lane4);
-            s[q][2] = col(a2, a3, a0, a1, k.z, lane4);
-            s[q][3] = col(a3, a0, a1, a2, k.w, lane4);
+            const uint4 k = lds_u128_v(rk.base + kRkRot + 32u);
+            s[q][0] = col_r(a0, a1, a2, a3, k.x, lane4);
+            s[q][1] = col_r(a1, a2, a3, a0, k.y, lane4);
+            s[q][2] = col_r(a2, a3, a0, a1, k.z, lane4);
+            s[q][3] = col_r(a3, a0, a1, a2, k.w, lane4);
         }
     }
     // two rounds per iteration: fully unrolled, the T-table code did not fit
@@ -117,13 +122,13 @@ __device__ __forceinline__ void t_half(uint32_t lane4, const RkLds& rk, const Ct
 #pragma unroll 2
 #endif
     for (int r = 3; r < NR; ++r) {
-        const uint4 k = rk.get(r);
+        const uint4 k = lds_u128_v(rk.base + kRkRot + 16u * r);   // rotr8 of round key r (col_r)
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
-            const uint32_t t0 = col(s[q][0], s[q][1], s[q][2], s[q][3], k.x, lane4);
-            const uint32_t t1 = col(s[q][1], s[q][2], s[q][3], s[q][0], k.y, lane4);
-            const uint32_t t2 = col(s[q][2], s[q][3], s[q][0], s[q][1], k.z, lane4);
-            const uint32_t t3 = col(s[q][3], s[q][0], s[q][1], s[q][2], k.w, lane4);
+            const uint32_t t0 = col_r(s[q][0], s[q][1], s[q][2], s[q][3], k.x, lane4);
+            const uint32_t t1 = col_r(s[q][1], s[q][2], s[q][3], s[q][0], k.y, lane4);
+            const uint32_t t2 = col_r(s[q][2], s[q][3], s[q][0], s[q][1], k.z, lane4);
+            const uint32_t t3 = col_r(s[q][3], s[q][0], s[q][1], s[q][2], k.w, lane4);
             s[q][0] = t0; s[q][1] = t1; s[q][2] = t2; s[q][3] = t3;
         }
     }
@@ -452,7 +457,7 @@ constexpr int kHyThreads = 1024;
 constexpr uint32_t kHySbox = 2 * 65536;
 constexpr uint32_t kHyRk = kHySbox + 256;               // 15 round keys (16 B each)
 constexpr uint32_t kHyJt = kHyRk + 256;                 // gmul_rot lane-offset rows
-constexpr uint32_t kHyKeys = kHyJt + 256;               // round-key planes (bs8::KeyPlanesLds)
+constexpr uint32_t kHyKeys = kHyJt + 256;               // round keys rotated right by 8 (kHyRk + kRkRot)
 constexpr uint32_t kHyRecBase = kHyKeys + 2048;
 constexpr size_t kHyLds = kHyRecBase + (kHyThreads / 64) * kRecArea;   // for either size
 static_assert(kTeBase == 65536, "Te block follows the GHASH tables");
@@ -474,7 +479,12 @@ __global__ __launch_bounds__(THREADS) void gcm_hy_kernel(const GcmKeyDev* __rest
     stage_ghash_rot(g_lds_bs8, key->ghash8, kHyJt);
     stage_te(reinterpret_cast<uint32_t*>(g_lds_bs8) + kTeBase / 4);
     stage_sbox(kHySbox);
-    if (threadIdx.x < 4 * (NR + 1)) reinterpret_cast<uint32_t*>(g_lds_bs8)[kHyRk / 4 + threadIdx.x] = key->rk[threadIdx.x];
+    static_assert(kHyRk + kRkRot == kHyKeys, "rotated round keys at kHyKeys");
+    if (threadIdx.x < 4 * (NR + 1)) {
+        const uint32_t w = key->rk[threadIdx.x];
+        reinterpret_cast<uint32_t*>(g_lds_bs8)[kHyRk / 4 + threadIdx.x] = w;
+        reinterpret_cast<uint32_t*>(g_lds_bs8)[kHyKeys / 4 + threadIdx.x] = rotl32(w, 24);
+    }
     __syncthreads();
     const uint32_t wave = (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
     const uint64_t njobs = (bp->n + 7) / 8;
