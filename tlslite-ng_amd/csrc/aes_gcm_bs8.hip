@@ -150,6 +150,8 @@ struct SingleKeyCtx {   // one key for the batch: 8-bit H^8 tables in LDS (gmul_
     __device__ __forceinline__ const uint32_t* rk() const { return key->rk; }
     __device__ __forceinline__ uint4 hpow(int e) const { return key->hpow[e - 1]; }
     __device__ __forceinline__ uint4 gmul(uint4 y) const { return gmul_rot(y, threadIdx.x & 15u, jt); }
+    // y * H^8 ^ x: Horner's step with the input folded into the XOR tree
+    __device__ __forceinline__ uint4 gmulx(uint4 y, uint4 x) const { return gmul_rot(y, threadIdx.x & 15u, jt, x); }
 };
 // SingleKeyCtx with the lane's offset row held in registers (the hybrid
 // kernel's waves of both roles: one ds_read_b128 fewer per block; T-table
@@ -160,6 +162,7 @@ struct SingleKeyRowCtx {
     __device__ __forceinline__ const uint32_t* rk() const { return key->rk; }
     __device__ __forceinline__ uint4 hpow(int e) const { return key->hpow[e - 1]; }
     __device__ __forceinline__ uint4 gmul(uint4 y) const { return gmul_rot_j(y, threadIdx.x & 15u, jw); }
+    __device__ __forceinline__ uint4 gmulx(uint4 y, uint4 x) const { return gmul_rot_j(y, threadIdx.x & 15u, jw, x); }
 };
 struct TableKeyCtx {    // a key of a key table: the wave's 4-bit H^8 tables in LDS (gmul4)
     const uint32_t* rkw;
@@ -171,6 +174,11 @@ struct TableKeyCtx {    // a key of a key table: the wave's 4-bit H^8 tables in 
     __device__ __forceinline__ uint4 gmul(uint4 y) const { return y; }
 #else
     __device__ __forceinline__ uint4 gmul(uint4 y) const { return gmul4(y, tab); }
+#endif
+#if defined(TG_KT_NO_GHASH)
+    __device__ __forceinline__ uint4 gmulx(uint4 y, uint4 x) const { return xor4(y, x); }
+#else
+    __device__ __forceinline__ uint4 gmulx(uint4 y, uint4 x) const { return gmul4(y, tab, x); }
 #endif
 };
 
@@ -251,7 +259,7 @@ __device__ __forceinline__ void octet_job(const KC& kc, const tg_batch& b,
     uint4 y = make_uint4(0, 0, 0, 0);
     for (uint32_t a = (l + na + nc + 1u) & kM; a < na; a += LPR) {
         const uint32_t m = alen - 16 * a < 16 ? alen - 16 * a : 16;
-        y = xor4(kc.gmul(y), load_partial(ad + 16 * a, m));
+        y = kc.gmulx(y, load_partial(ad + 16 * a, m));
     }
 
     // the bitsliced cipher leaves out the last round key (folded into the XOR)
@@ -278,7 +286,7 @@ __device__ __forceinline__ void octet_job(const KC& kc, const tg_batch& b,
                     if (!OPEN) d[q] = c;
                 }
 #pragma unroll
-                for (int q = 0; q < N; ++q) y = xor4(kc.gmul(y), d[q]);
+                for (int q = 0; q < N; ++q) y = kc.gmulx(y, d[q]);
             }
         } else {
 #pragma unroll
@@ -297,7 +305,7 @@ __device__ __forceinline__ void octet_job(const KC& kc, const tg_batch& b,
                     c = mask_tail(xor4(d, kk), tail);
                     store_partial(out + 16u * blk, c, tail);
                 }
-                y = xor4(kc.gmul(y), OPEN ? d : c);
+                y = kc.gmulx(y, OPEN ? d : c);
             }
         }
     };
@@ -384,7 +392,7 @@ __device__ __forceinline__ void octet_job(const KC& kc, const tg_batch& b,
     // length block be64(8 alen) || be64(8 len) (aesgcm.py:64): the last position
     if (l == kM) {
         const uint64_t abits = (uint64_t)alen << 3, cbits = (uint64_t)len << 3;
-        y = xor4(kc.gmul(y), make_uint4(bswap32((uint32_t)(abits >> 32)), bswap32((uint32_t)abits),
+        y = kc.gmulx(y, make_uint4(bswap32((uint32_t)(abits >> 32)), bswap32((uint32_t)abits),
                                      bswap32((uint32_t)(cbits >> 32)), bswap32((uint32_t)cbits)));
     }
     // lift by H^(LPR - l) and XOR-reduce over the record's lanes

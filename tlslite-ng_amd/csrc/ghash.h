@@ -84,7 +84,10 @@ __device__ __forceinline__ uint32_t sel32(uint32_t m, uint32_t t, uint32_t f) { 
     return (m & t) | (~m & f);
 #endif
 }
-__device__ __forceinline__ uint4 gmul_rot_j(uint4 y, uint32_t lane16, uint4 jw) {
+// acc: XORed into the product (y * H ^ acc, Horner's next input) as the first
+// level of the XOR tree -- no separate four XORs per block.
+__device__ __forceinline__ uint4 gmul_rot_j(uint4 y, uint32_t lane16, uint4 jw,
+                                            uint4 acc = make_uint4(0, 0, 0, 0)) {
     const uint32_t m8 = 0u - ((lane16 >> 3) & 1u), m4 = 0u - ((lane16 >> 2) & 1u);
     const uint32_t h0 = sel32(m8, y.z, y.x), h1 = sel32(m8, y.w, y.y);
     const uint32_t h2 = sel32(m8, y.x, y.z), h3 = sel32(m8, y.y, y.w);
@@ -94,7 +97,7 @@ __device__ __forceinline__ uint4 gmul_rot_j(uint4 y, uint32_t lane16, uint4 jw) 
     const uint32_t v[4] = {__builtin_amdgcn_alignbit(u1, u0, s8), __builtin_amdgcn_alignbit(u2, u1, s8),
                            __builtin_amdgcn_alignbit(u3, u2, s8), __builtin_amdgcn_alignbit(u0, u3, s8)};
     const uint32_t j[4] = {jw.x, jw.y, jw.z, jw.w};
-    uint4 z = make_uint4(0, 0, 0, 0);
+    uint4 z = acc;
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
         uint4 e[8];
@@ -113,8 +116,9 @@ __device__ __forceinline__ uint4 gmul_rot_j(uint4 y, uint32_t lane16, uint4 jw) 
 }
 
 // gmul_rot with the lane-offset row read from LDS per multiply.
-__device__ __forceinline__ uint4 gmul_rot(uint4 y, uint32_t lane16, uint32_t jt) {
-    return gmul_rot_j(y, lane16, lds_u128(jt + (lane16 << 4)));
+__device__ __forceinline__ uint4 gmul_rot(uint4 y, uint32_t lane16, uint32_t jt,
+                                          uint4 acc = make_uint4(0, 0, 0, 0)) {
+    return gmul_rot_j(y, lane16, lds_u128(jt + (lane16 << 4)), acc);
 }
 
 // Stage the 8-bit tables of ``src`` (GcmKeyDev layout, entry (j, b) at
@@ -262,9 +266,9 @@ __device__ __forceinline__ void build_table4(uint32_t tab, uint4 gn) {
 
 // y * G through the 4-bit tables at ``tab`` (32 lookups, no reduction).
 // tab must be 256-byte aligned (the nibble offsets are ORed in).
-__device__ __forceinline__ uint4 gmul4(uint4 y, uint32_t tab) {
+__device__ __forceinline__ uint4 gmul4(uint4 y, uint32_t tab, uint4 acc = make_uint4(0, 0, 0, 0)) {
     const uint32_t w[4] = {y.x, y.y, y.z, y.w};
-    uint4 z = make_uint4(0, 0, 0, 0);
+    uint4 z = acc;   // y * G ^ acc (see gmul_rot_j)
     // the nibble mask in a VGPR: (x & m) | tab is then one full-rate
     // v_bitop3 (an SGPR or literal operand makes it half rate or two ops)
     uint32_t m = 0xf0u;
