@@ -266,17 +266,40 @@ TG_BS_HD void mix_round_folded(uint32_t (*s)[8], const KM& km, int r) {
 // 8 x 8 bit transpose inside every byte of a[0..7]: bit j of byte c of a[b]
 // <-> bit b of byte c of a[j] (three swap stages, two shifts + two bitop3
 // per pair).
-TG_BS_HD void transpose8(uint32_t* a) {
+// The stage masks in VGPRs: as SGPR or literal operands they make every
+// v_bitop3 of the transposes half rate (VOP3 with a scalar operand), 96 of
+// them per batch of eight blocks.  mask << m is ~mask, so one mask per stage
+// serves both selects (operands swapped).
+struct TransposeMasks {
+    uint32_t m4, m2, m1;   // 0x0f0f0f0f, 0x33333333, 0x55555555
+};
+TG_BS_HD TransposeMasks transpose_masks() {
+    TransposeMasks t{0x0f0f0f0fu, 0x33333333u, 0x55555555u};
+#if defined(__HIP_DEVICE_COMPILE__)
+    asm volatile("v_mov_b32 %0, 0x0f0f0f0f" : "=v"(t.m4));
+    asm volatile("v_mov_b32 %0, 0x33333333" : "=v"(t.m2));
+    asm volatile("v_mov_b32 %0, 0x55555555" : "=v"(t.m1));
+#endif
+    return t;
+}
+
+TG_BS_HD void transpose8(uint32_t* a, const TransposeMasks& tm) {
 #pragma unroll
     for (int l = 2; l >= 0; --l) {
         const int m = 1 << l;
-        const uint32_t mask = m == 4 ? 0x0f0f0f0fu : m == 2 ? 0x33333333u : 0x55555555u;
+        const uint32_t mask = m == 4 ? tm.m4 : m == 2 ? tm.m2 : tm.m1;
 #pragma unroll
         for (int r = 0; r < 8; ++r) {
             if (r & m) continue;
             const uint32_t x = a[r], y = a[r + m];
-            a[r] = bop3(mask << m, y << m, x, 0xca);   // (y << m) where mask << m, else x
-            a[r + m] = bop3(mask, x >> m, y, 0xca);    // (x >> m) where mask, else y
+            // y << 1 as y + y: v_lshlrev_b32 issues at half rate, v_add_u32 at
+            // full (in asm: the compiler turns y + y back into a shift)
+            uint32_t ys = y << m;
+#if defined(__HIP_DEVICE_COMPILE__)
+            if (m == 1) asm("v_add_u32 %0, %1, %1" : "=v"(ys) : "v"(y));
+#endif
+            a[r] = bop3(mask, x, ys, 0xca);           // (y << m) where ~mask, else x
+            a[r + m] = bop3(mask, x >> m, y, 0xca);   // (x >> m) where mask, else y
         }
     }
 }
@@ -300,9 +323,10 @@ TG_BS_HD void to_blocks(uint32_t (*x)[8], uint32_t (*w)[8]) {
         w[3][b] = perm(B2, A2, 0x07060302u);
         TG_BS8_FENCE();
     }
+    const TransposeMasks tm = transpose_masks();
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
-        transpose8(w[q]);
+        transpose8(w[q], tm);
         TG_BS8_FENCE();
     }
 }

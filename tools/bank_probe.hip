@@ -62,6 +62,42 @@ __global__ __launch_bounds__(512) void probe3(unsigned* out, int iters) {
     if (threadIdx.x == 0) out[blockIdx.x] = iters;
 }
 
+// v_perm_b32 / v_bitop3_b32 with the third operand in an SGPR vs a VGPR
+template <int K>
+__global__ __launch_bounds__(512) void probe_sop(unsigned* out, int iters, unsigned sel) {
+    for (int i = 0; i < iters; ++i) {
+        if (K == 0)
+            asm volatile(".rept 32\n"
+                         "v_perm_b32 v10, v20, v21, %0\n v_perm_b32 v11, v21, v22, %0\n"
+                         "v_perm_b32 v12, v22, v23, %0\n v_perm_b32 v13, v23, v24, %0\n"
+                         "v_perm_b32 v14, v24, v25, %0\n v_perm_b32 v15, v25, v26, %0\n"
+                         "v_perm_b32 v16, v26, v27, %0\n v_perm_b32 v17, v27, v20, %0\n"
+                         ".endr\n" :: "s"(sel) : CLOB);
+        if (K == 1)
+            asm volatile("v_mov_b32 v28, %0\n.rept 32\n"
+                         "v_perm_b32 v10, v20, v21, v28\n v_perm_b32 v11, v21, v22, v28\n"
+                         "v_perm_b32 v12, v22, v23, v28\n v_perm_b32 v13, v23, v24, v28\n"
+                         "v_perm_b32 v14, v24, v25, v28\n v_perm_b32 v15, v25, v26, v28\n"
+                         "v_perm_b32 v16, v26, v27, v28\n v_perm_b32 v17, v27, v20, v28\n"
+                         ".endr\n" :: "s"(sel) : CLOB, "v28");
+        if (K == 2)
+            asm volatile(".rept 32\n"
+                         "v_bitop3_b32 v10, v20, v21, %0 bitop3:0xca\n v_bitop3_b32 v11, v21, v22, %0 bitop3:0xca\n"
+                         "v_bitop3_b32 v12, v22, v23, %0 bitop3:0xca\n v_bitop3_b32 v13, v23, v24, %0 bitop3:0xca\n"
+                         "v_bitop3_b32 v14, v24, v25, %0 bitop3:0xca\n v_bitop3_b32 v15, v25, v26, %0 bitop3:0xca\n"
+                         "v_bitop3_b32 v16, v26, v27, %0 bitop3:0xca\n v_bitop3_b32 v17, v27, v20, %0 bitop3:0xca\n"
+                         ".endr\n" :: "s"(sel) : CLOB);
+        if (K == 3)
+            asm volatile("v_mov_b32 v28, %0\n.rept 32\n"
+                         "v_bitop3_b32 v10, v20, v21, v28 bitop3:0xca\n v_bitop3_b32 v11, v21, v22, v28 bitop3:0xca\n"
+                         "v_bitop3_b32 v12, v22, v23, v28 bitop3:0xca\n v_bitop3_b32 v13, v23, v24, v28 bitop3:0xca\n"
+                         "v_bitop3_b32 v14, v24, v25, v28 bitop3:0xca\n v_bitop3_b32 v15, v25, v26, v28 bitop3:0xca\n"
+                         "v_bitop3_b32 v16, v26, v27, v28 bitop3:0xca\n v_bitop3_b32 v17, v27, v20, v28 bitop3:0xca\n"
+                         ".endr\n" :: "s"(sel) : CLOB, "v28");
+    }
+    if (threadIdx.x == 0) out[blockIdx.x] = iters;
+}
+
 template <class F>
 float timeit(F f) {
     hipEvent_t a, b;
@@ -98,6 +134,10 @@ int main() {
         rep("v_alignbit same-bank sources", timeit([&] { probe3<0><<<blocks, 512>>>(out, iters); }));
         rep("v_alignbit different-bank sources", timeit([&] { probe3<1><<<blocks, 512>>>(out, iters); }));
         rep("v_alignbit one source twice", timeit([&] { probe3<2><<<blocks, 512>>>(out, iters); }));
+        rep("v_perm selector in an SGPR", timeit([&] { probe_sop<0><<<blocks, 512>>>(out, iters, 0x05040100u); }));
+        rep("v_perm selector in a VGPR", timeit([&] { probe_sop<1><<<blocks, 512>>>(out, iters, 0x05040100u); }));
+        rep("v_bitop3 third operand in an SGPR", timeit([&] { probe_sop<2><<<blocks, 512>>>(out, iters, 0x0f0f0f0fu); }));
+        rep("v_bitop3 third operand in a VGPR", timeit([&] { probe_sop<3><<<blocks, 512>>>(out, iters, 0x0f0f0f0fu); }));
     }
     return 0;
 }
