@@ -78,10 +78,10 @@ __device__ __forceinline__ uint32_t wave_min_u32(uint32_t v) {
 // a window in this batch (a wave-uniform test), else full rounds.  Round keys
 // are read from LDS (wave-uniform address: one broadcast ds_read_b128 per
 // round), which keeps the 44 / 60 key words out of the SGPR file.
-// The hybrid kernel keeps its round keys rotated right by 8 bits kRkRot bytes
-// past the plain ones (RkLds base): the T-table columns of rounds 2 .. NR - 1
-// take them inside the rotation (aes_round.h col_r, one XOR per column fewer).
-constexpr uint32_t kRkRot = 512;
+// The hybrid kernel's T-table columns of rounds 2 .. NR - 1 take the round keys
+// rotated right by 8 bits (aes_round.h col_r, one XOR per column fewer), from
+// a wave-uniform global copy the setup kernel writes (RkLds::rot: scalar
+// loads, so the LDS pipe the T-table waves are bound by carries no key reads).
 
 template <int NR>
 __device__ __forceinline__ void t_half(uint32_t lane4, const RkLds& rk, const CtrCache& cc,
@@ -103,7 +103,7 @@ __device__ __forceinline__ void t_half(uint32_t lane4, const RkLds& rk, const Ct
             const uint32_t a1 = cc.k1 ^ T2<2>(s3, lane4);
             const uint32_t a2 = cc.k2 ^ rotl32(T0<1>(s3, lane4), 8);
             const uint32_t a3 = cc.k3 ^ T0<0>(s3, lane4);
-            const uint4 k = lds_u128_v(rk.base + kRkRot + 32u);
+            const uint4 k = rk.rot[2];
             s[q][0] = col_r(a0, a1, a2, a3, k.x, lane4);
             s[q][1] = col_r(a1, a2, a3, a0, k.y, lane4);
             s[q][2] = col_r(a2, a3, a0, a1, k.z, lane4);
@@ -122,7 +122,7 @@ __device__ __forceinline__ void t_half(uint32_t lane4, const RkLds& rk, const Ct
 #pragma unroll 2
 #endif
     for (int r = 3; r < NR; ++r) {
-        const uint4 k = lds_u128_v(rk.base + kRkRot + 16u * r);   // rotr8 of round key r (col_r)
+        const uint4 k = rk.rot[r];   // rotr8 of round key r (col_r), scalar loads
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
             const uint32_t t0 = col_r(s[q][0], s[q][1], s[q][2], s[q][3], k.x, lane4);
@@ -465,7 +465,7 @@ constexpr int kHyThreads = 1024;
 constexpr uint32_t kHySbox = 2 * 65536;
 constexpr uint32_t kHyRk = kHySbox + 256;               // 15 round keys (16 B each)
 constexpr uint32_t kHyJt = kHyRk + 256;                 // gmul_rot lane-offset rows
-constexpr uint32_t kHyKeys = kHyJt + 256;               // round keys rotated right by 8 (kHyRk + kRkRot)
+constexpr uint32_t kHyKeys = kHyJt + 256;               // (unused: round 2's key-plane area)
 constexpr uint32_t kHyRecBase = kHyKeys + 2048;
 constexpr size_t kHyLds = kHyRecBase + (kHyThreads / 64) * kRecArea;   // for either size
 static_assert(kTeBase == 65536, "Te block follows the GHASH tables");
@@ -483,16 +483,12 @@ __global__ __launch_bounds__(THREADS) void gcm_hy_kernel(const GcmKeyDev* __rest
                                                             const uint32_t* __restrict__ order,
                                                             uint32_t* __restrict__ queue,
                                                             uint32_t nt, uint32_t prio,
-                                                            const uint4* __restrict__ krows) {
+                                                            const uint4* __restrict__ krows,
+                                                            const uint4* __restrict__ rkrot) {
     stage_ghash_rot(g_lds_bs8, key->ghash8, kHyJt);
     stage_te(reinterpret_cast<uint32_t*>(g_lds_bs8) + kTeBase / 4);
     stage_sbox(kHySbox);
-    static_assert(kHyRk + kRkRot == kHyKeys, "rotated round keys at kHyKeys");
-    if (threadIdx.x < 4 * (NR + 1)) {
-        const uint32_t w = key->rk[threadIdx.x];
-        reinterpret_cast<uint32_t*>(g_lds_bs8)[kHyRk / 4 + threadIdx.x] = w;
-        reinterpret_cast<uint32_t*>(g_lds_bs8)[kHyKeys / 4 + threadIdx.x] = rotl32(w, 24);
-    }
+    if (threadIdx.x < 4 * (NR + 1)) reinterpret_cast<uint32_t*>(g_lds_bs8)[kHyRk / 4 + threadIdx.x] = key->rk[threadIdx.x];
     __syncthreads();
     const uint32_t wave = (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
     const uint64_t njobs = (bp->n + 7) / 8;
@@ -500,7 +496,7 @@ __global__ __launch_bounds__(THREADS) void gcm_hy_kernel(const GcmKeyDev* __rest
     const uint4 jw = lds_u128(kHyJt + ((threadIdx.x & 15u) << 4));
     if (wave < nt) {
         if (prio) __builtin_amdgcn_s_setprio(1);
-        const RkLds rk{kHyRk};
+        const RkLds rk{kHyRk, rkrot};
         for (;;) {
             uint32_t job = 0;
             if ((threadIdx.x & 63u) == 0) job = atomicAdd(queue, 1u);
@@ -532,7 +528,9 @@ __global__ __launch_bounds__(THREADS) void gcm_hy_kernel(const GcmKeyDev* __rest
 // The rows hold the bs8_fold_word planes (KeyPlanesVmemFolded) for rounds
 // 1 .. nr - 1 and the round-key planes for rounds 0 and nr.
 __global__ void hy_setup_kernel(tg_batch b, uint32_t* queue, tg_batch* bcopy,
-                                const GcmKeyDev* __restrict__ key, uint32_t* krows, int nr) {
+                                const GcmKeyDev* __restrict__ key, uint32_t* krows, int nr,
+                                uint32_t* rkrot) {
+    for (int e = threadIdx.x; e < 4 * (nr + 1); e += blockDim.x) rkrot[e] = rotl32(key->rk[e], 24);
     if (threadIdx.x == 0) {
         *queue = 0;
         *bcopy = b;
@@ -573,19 +571,22 @@ int launch_hy(const GcmKeyDev* key, const tg_batch& b, hipStream_t s, const uint
     // job counter + batch copy + key rows: stream-ordered scratch, so
     // concurrent batches never share them
     uint8_t* scratch = nullptr;
-    if (hipMallocAsync((void**)&scratch, 256 + 2048, s) != hipSuccess) return TG_EHIP;
+    if (hipMallocAsync((void**)&scratch, 256 + 2048 + 256, s) != hipSuccess) return TG_EHIP;
     uint32_t* queue = reinterpret_cast<uint32_t*>(scratch);
     tg_batch* bcopy = reinterpret_cast<tg_batch*>(scratch + 64);
     uint32_t* krows = reinterpret_cast<uint32_t*>(scratch + 256);
-    hipLaunchKernelGGL(hy_setup_kernel, dim3(1), dim3(64), 0, s, b, queue, bcopy, key, krows, NR);
+    uint32_t* rkrot = reinterpret_cast<uint32_t*>(scratch + 256 + 2048);   // col_r keys
+    hipLaunchKernelGGL(hy_setup_kernel, dim3(1), dim3(64), 0, s, b, queue, bcopy, key, krows, NR, rkrot);
     bool ok = hipGetLastError() == hipSuccess;
     if (ok) {
         if (small)
             hipLaunchKernelGGL((gcm_hy_kernel<NR, OPEN, 768>), dim3((unsigned)device_cus()), dim3(768), kHyLds, s,
-                               key, (const tg_batch*)bcopy, order, queue, nt, prio, (const uint4*)krows);
+                               key, (const tg_batch*)bcopy, order, queue, nt, prio, (const uint4*)krows,
+                               (const uint4*)rkrot);
         else
             hipLaunchKernelGGL((gcm_hy_kernel<NR, OPEN, 1024>), dim3((unsigned)device_cus()), dim3(1024), kHyLds,
-                               s, key, (const tg_batch*)bcopy, order, queue, nt, prio, (const uint4*)krows);
+                               s, key, (const tg_batch*)bcopy, order, queue, nt, prio, (const uint4*)krows,
+                               (const uint4*)rkrot);
         ok = hipGetLastError() == hipSuccess;
     }
     if (hipFreeAsync(scratch, s) != hipSuccess) return TG_EHIP;

@@ -135,6 +135,7 @@ struct RkRegs {  // single key per launch: wave-uniform, lives in SGPRs
 };
 struct RkLds {  // key table: this lane's schedule staged in an LDS row
     uint32_t base;
+    const uint4* rot = nullptr;   // hybrid AES-GCM: round keys rotated right by 8 (global, wave-uniform)
     // volatile: re-read per round instead of being hoisted into 60 VGPRs
     __device__ __forceinline__ uint4 get(int r) const { return lds_u128_v(base + 16 * r); }
 };
