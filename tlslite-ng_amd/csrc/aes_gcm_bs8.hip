@@ -132,7 +132,7 @@ __device__ __forceinline__ void t_half(uint32_t lane4, const RkLds& rk, const Ct
             s[q][0] = t0; s[q][1] = t1; s[q][2] = t2; s[q][3] = t3;
         }
     }
-    const uint4 k = rk.get(NR);
+    const uint4 k = rk.rot[NR + 1];   // the plain last round key, after the rotated ones
 #pragma unroll
     for (int q = 0; q < 4; ++q)
         ks[q] = make_uint4(col_last(s[q][0], s[q][1], s[q][2], s[q][3], k.x, lane4),
@@ -530,7 +530,8 @@ __global__ __launch_bounds__(THREADS) void gcm_hy_kernel(const GcmKeyDev* __rest
 __global__ void hy_setup_kernel(tg_batch b, uint32_t* queue, tg_batch* bcopy,
                                 const GcmKeyDev* __restrict__ key, uint32_t* krows, int nr,
                                 uint32_t* rkrot) {
-    for (int e = threadIdx.x; e < 4 * (nr + 1); e += blockDim.x) rkrot[e] = rotl32(key->rk[e], 24);
+    for (int e = threadIdx.x; e < 4 * (nr + 2); e += blockDim.x)   // + the plain last key
+        rkrot[e] = e < 4 * (nr + 1) ? rotl32(key->rk[e], 24) : key->rk[e - 4];
     if (threadIdx.x == 0) {
         *queue = 0;
         *bcopy = b;
