@@ -23,7 +23,7 @@
  * the reference's T-table lookups (rijndael.py:1016-1022) encode.          */
 
 static uint8_t g_sbox[256];
-static pthread_once_t g_sbox_once = PTHREAD_ONCE_INIT;
+static pthread_once_t g_tables_once = PTHREAD_ONCE_INIT;
 
 static uint8_t gf_mul(uint8_t a, uint8_t b) {
     uint8_t p = 0;
@@ -55,11 +55,15 @@ static void build_sbox(void) {
 typedef struct {
     int rounds;
     uint8_t rk[15][16];
+    uint32_t rkw[15][4];  /* the same round keys as big-endian column words */
 } aes_ctx;
+
+static uint32_t g_te[4][256];
+static void build_tables(void);
 
 /* Key expansion, rijndael.py:922-993 (Nk = keylen/4, Nr = 10/12/14). */
 static int aes_setup(aes_ctx* c, const uint8_t* key, size_t keylen) {
-    pthread_once(&g_sbox_once, build_sbox);
+    pthread_once(&g_tables_once, build_tables);
     if (keylen != 16 && keylen != 24 && keylen != 32) return -1;
     int nk = (int)keylen / 4;
     c->rounds = nk + 6;
@@ -83,12 +87,59 @@ static int aes_setup(aes_ctx* c, const uint8_t* key, size_t keylen) {
         for (int k = 0; k < 4; ++k) w[i][k] = (uint8_t)(w[i - nk][k] ^ t[k]);
     }
     for (int r = 0; r <= c->rounds; ++r)
-        for (int j = 0; j < 4; ++j) memcpy(&c->rk[r][4 * j], w[4 * r + j], 4);
+        for (int j = 0; j < 4; ++j) {
+            memcpy(&c->rk[r][4 * j], w[4 * r + j], 4);
+            c->rkw[r][j] = ((uint32_t)w[4 * r + j][0] << 24) | ((uint32_t)w[4 * r + j][1] << 16) |
+                           ((uint32_t)w[4 * r + j][2] << 8) | w[4 * r + j][3];
+        }
     return 0;
 }
 
-/* Rijndael.encrypt, rijndael.py:995-1038. */
+/* Rijndael.encrypt, rijndael.py:995-1038, as the reference evaluates it:
+ * big-endian column words, 9 (or 13) rounds of four T-table lookups per
+ * column (rijndael.py:1016-1022, tables T1-T4 of :118-377), and a final
+ * S-box round (:1024-1038).  The tables are derived here from the S-box
+ * (T1[x] = (2s, s, s, 3s) big-endian, T2..T4 its byte rotations), exactly
+ * the products rijndael.py's tables hold.  aes_encrypt_bytes() below is the
+ * same cipher as SubBytes/ShiftRows/MixColumns on bytes; oracle_selfcheck()
+ * compares the two on random blocks. */
+static void build_tables(void) {
+    build_sbox();
+    for (int x = 0; x < 256; ++x) {
+        uint32_t s = g_sbox[x], s2 = gf_mul((uint8_t)s, 2), s3 = s2 ^ s;
+        uint32_t w = (s2 << 24) | (s << 16) | (s << 8) | s3;
+        for (int t = 0; t < 4; ++t) g_te[t][x] = t ? (w >> (8 * t)) | (w << (32 - 8 * t)) : w;
+    }
+}
+
+static uint32_t be32(const uint8_t* p) {
+    return ((uint32_t)p[0] << 24) | ((uint32_t)p[1] << 16) | ((uint32_t)p[2] << 8) | p[3];
+}
+
 static void aes_encrypt(const aes_ctx* c, const uint8_t in[16], uint8_t out[16]) {
+    uint32_t s[4], t[4];
+    for (int j = 0; j < 4; ++j) s[j] = be32(in + 4 * j) ^ c->rkw[0][j];
+    for (int r = 1; r < c->rounds; ++r) {
+        for (int j = 0; j < 4; ++j)
+            t[j] = g_te[0][s[j] >> 24] ^ g_te[1][(s[(j + 1) & 3] >> 16) & 0xff] ^
+                   g_te[2][(s[(j + 2) & 3] >> 8) & 0xff] ^ g_te[3][s[(j + 3) & 3] & 0xff] ^
+                   c->rkw[r][j];
+        for (int j = 0; j < 4; ++j) s[j] = t[j];
+    }
+    for (int j = 0; j < 4; ++j) {
+        uint32_t w = ((uint32_t)g_sbox[s[j] >> 24] << 24) |
+                     ((uint32_t)g_sbox[(s[(j + 1) & 3] >> 16) & 0xff] << 16) |
+                     ((uint32_t)g_sbox[(s[(j + 2) & 3] >> 8) & 0xff] << 8) |
+                     g_sbox[s[(j + 3) & 3] & 0xff];
+        w ^= c->rkw[c->rounds][j];
+        out[4 * j] = (uint8_t)(w >> 24); out[4 * j + 1] = (uint8_t)(w >> 16);
+        out[4 * j + 2] = (uint8_t)(w >> 8); out[4 * j + 3] = (uint8_t)w;
+    }
+}
+
+/* The same cipher as SubBytes + ShiftRows + MixColumns on bytes (FIPS-197
+ * 5.1); used only by oracle_selfcheck() to cross-check the table form. */
+static void aes_encrypt_bytes(const aes_ctx* c, const uint8_t in[16], uint8_t out[16]) {
     uint8_t s[16];
     for (int i = 0; i < 16; ++i) s[i] = (uint8_t)(in[i] ^ c->rk[0][i]);
     for (int r = 1; r <= c->rounds; ++r) {
@@ -157,28 +208,28 @@ static u128 gcm_shift(u128 x) {  /* AESGCM._gcmShift, aesgcm.py:168-178 */
 
 typedef struct {
     aes_ctx aes;
-    u128 table[16];  /* 4-bit multiples of H, aesgcm.py:46-57 */
+    u128 table[16];   /* 4-bit multiples of H, aesgcm.py:46-57 */
+    u128 table8[256]; /* the same products a byte at a time (see gcm_mul) */
 } gcm_ctx;
 
-static int gcm_setup(gcm_ctx* g, const uint8_t* key, size_t keylen) {
-    if (keylen != 16 && keylen != 32) return -1;  /* aesgcm.py:33-38 */
-    if (aes_setup(&g->aes, key, keylen)) return -1;
-    uint8_t zero[16] = {0}, hb[16];
-    aes_encrypt(&g->aes, zero, hb);                  /* H = E_K(0), :45 */
-    u128 h = load_be128(hb);
-    memset(g->table, 0, sizeof(g->table));
-    g->table[rev4(1)] = h;
-    for (unsigned i = 2; i < 16; i += 2) {
-        g->table[rev4(i)] = gcm_shift(g->table[rev4(i / 2)]);
-        u128 t = g->table[rev4(i)];
-        t.hi ^= h.hi; t.lo ^= h.lo;
-        g->table[rev4(i + 1)] = t;
+/* Reduction of the byte shifted out by y*x^8 (the 8-bit widening of the
+ * reference's _gcmReductionTable, aesgcm.py:190-193: bit i of the byte is the
+ * coefficient of x^(127-i) and folds back as x^(7-i) * (1 + x + x^2 + x^7)). */
+static uint16_t g_red8[256];
+static pthread_once_t g_red8_once = PTHREAD_ONCE_INIT;
+
+static void build_red8(void) {
+    for (unsigned b = 0; b < 256; ++b) {
+        uint16_t r = 0;
+        for (int i = 0; i < 8; ++i)
+            if (b & (1u << i)) r ^= (uint16_t)(0xe100 >> (7 - i));
+        g_red8[b] = r;
     }
-    return 0;
 }
 
-/* AESGCM._mul, aesgcm.py:81-99: y*H, four bits at a time. */
-static u128 gcm_mul(const gcm_ctx* g, u128 y) {
+/* AESGCM._mul, aesgcm.py:81-99: y*H, four bits at a time (the reference's
+ * own formulation; oracle_selfcheck() compares gcm_mul with it). */
+static u128 gcm_mul4(const gcm_ctx* g, u128 y) {
     u128 ret = {0, 0};
     for (int i = 0; i < 32; ++i) {
         unsigned high = (unsigned)(ret.lo & 0xf);
@@ -189,6 +240,58 @@ static u128 gcm_mul(const gcm_ctx* g, u128 y) {
         ret.hi ^= p.hi; ret.lo ^= p.lo;
         y.lo = (y.lo >> 4) | (y.hi << 60);
         y.hi >>= 4;
+    }
+    return ret;
+}
+
+static void gcm_set_h(gcm_ctx* g, u128 h);
+
+static int gcm_setup(gcm_ctx* g, const uint8_t* key, size_t keylen) {
+    if (keylen != 16 && keylen != 32) return -1;  /* aesgcm.py:33-38 */
+    if (aes_setup(&g->aes, key, keylen)) return -1;
+    uint8_t zero[16] = {0}, hb[16];
+    aes_encrypt(&g->aes, zero, hb);                  /* H = E_K(0), :45 */
+    gcm_set_h(g, load_be128(hb));
+    return 0;
+}
+
+/* The product tables of H (aesgcm.py:46-57). */
+static void gcm_set_h(gcm_ctx* g, u128 h) {
+    pthread_once(&g_red8_once, build_red8);
+    memset(g->table, 0, sizeof(g->table));
+    g->table[rev4(1)] = h;
+    for (unsigned i = 2; i < 16; i += 2) {
+        g->table[rev4(i)] = gcm_shift(g->table[rev4(i / 2)]);
+        u128 t = g->table[rev4(i)];
+        t.hi ^= h.hi; t.lo ^= h.lo;
+        g->table[rev4(i + 1)] = t;
+    }
+    /* table8[b] = H * (b at the top byte): bit 7 of b is x^0, bit 0 is x^7,
+     * so table8[0x80 >> k] = H * x^k, and the rest follow by linearity. */
+    u128 basis[8];
+    basis[0] = h;
+    for (int k = 1; k < 8; ++k) basis[k] = gcm_shift(basis[k - 1]);
+    for (unsigned b = 0; b < 256; ++b) {
+        u128 t = {0, 0};
+        for (int k = 0; k < 8; ++k)
+            if (b & (0x80u >> k)) { t.hi ^= basis[k].hi; t.lo ^= basis[k].lo; }
+        g->table8[b] = t;
+    }
+}
+
+/* y*H a byte at a time: the Horner loop of AESGCM._mul (aesgcm.py:86-97) with
+ * eight-bit digits instead of four. */
+static u128 gcm_mul(const gcm_ctx* g, u128 y) {
+    u128 ret = {0, 0};
+    for (int i = 0; i < 16; ++i) {
+        unsigned high = (unsigned)(ret.lo & 0xff);
+        ret.lo = (ret.lo >> 8) | (ret.hi << 56);
+        ret.hi >>= 8;
+        ret.hi ^= (uint64_t)g_red8[high] << 48;
+        u128 p = g->table8[y.lo & 0xff];
+        ret.hi ^= p.hi; ret.lo ^= p.lo;
+        y.lo = (y.lo >> 8) | (y.hi << 56);
+        y.hi >>= 8;
     }
     return ret;
 }
@@ -225,6 +328,19 @@ static void gcm_auth(const gcm_ctx* g, const uint8_t* ct, size_t ctlen,
     u128 m = load_be128(mask);
     y.hi ^= m.hi; y.lo ^= m.lo;
     store_be128(y, tag);
+}
+
+/* AESGCM._auth without the tag mask, for a given H: the GHASH value the
+ * reference's _auth returns before the XOR with E_K(J0) (aesgcm.py:60-67). */
+void oracle_ghash(const uint8_t h[16], const uint8_t* aad, size_t aadlen,
+                  const uint8_t* ct, size_t ctlen, uint8_t out[16]) {
+    static gcm_ctx g;   /* 4.3 KiB of tables: keep them off the caller's stack */
+    static pthread_mutex_t mu = PTHREAD_MUTEX_INITIALIZER;
+    uint8_t zero[16] = {0};
+    pthread_mutex_lock(&mu);
+    gcm_set_h(&g, load_be128(h));
+    gcm_auth(&g, ct, ctlen, aad, aadlen, zero, out);
+    pthread_mutex_unlock(&mu);
 }
 
 /* Python_AES_CTR.encrypt with a full 128-bit big-endian counter increment
@@ -702,4 +818,33 @@ int oracle_batch(int alg, int op, const uint8_t* keys, size_t keylen,
     for (int t = 0; t < nthreads; ++t)
         if (jobs[t].rc) return -1;
     return 0;
+}
+
+/* ------------------------------------------------------------ self-check --
+ * The fast forms above against the reference's own formulations: the T-table
+ * cipher against SubBytes/ShiftRows/MixColumns on bytes, and the byte-wise
+ * GHASH multiply against the nibble-wise AESGCM._mul.  Returns the number of
+ * mismatches over n random (key, block) pairs. */
+static uint64_t xs64(uint64_t* s) {
+    *s ^= *s << 13; *s ^= *s >> 7; *s ^= *s << 17;
+    return *s;
+}
+
+int oracle_selfcheck(size_t n, uint64_t seed) {
+    int bad = 0;
+    uint64_t s = seed | 1;
+    for (size_t i = 0; i < n; ++i) {
+        uint8_t key[32], blk[16], a[16], b[16];
+        for (int k = 0; k < 32; ++k) key[k] = (uint8_t)xs64(&s);
+        for (int k = 0; k < 16; ++k) blk[k] = (uint8_t)xs64(&s);
+        gcm_ctx g;
+        gcm_setup(&g, key, (i & 1) ? 32 : 16);
+        aes_encrypt(&g.aes, blk, a);
+        aes_encrypt_bytes(&g.aes, blk, b);
+        bad += memcmp(a, b, 16) != 0;
+        u128 y = load_be128(blk);
+        u128 p = gcm_mul(&g, y), q = gcm_mul4(&g, y);
+        bad += (p.hi != q.hi) || (p.lo != q.lo);
+    }
+    return bad;
 }

@@ -78,6 +78,16 @@ int oracle_batch(int alg, int op, const uint8_t* keys, size_t keylen,
                  const uint64_t* out_off, uint8_t* status, size_t n,
                  int nthreads);
 
+/* GHASH_H(aad, ct) with the length block, i.e. AESGCM._auth before the tag
+ * mask (aesgcm.py:60-67), for an arbitrary H (16 bytes, big-endian). */
+void oracle_ghash(const uint8_t h[16], const uint8_t* aad, size_t aadlen,
+                  const uint8_t* ct, size_t ctlen, uint8_t out[16]);
+
+/* Cross-check of the oracle's fast forms against the reference's own
+ * formulations (T-table AES vs byte-wise rounds, byte-wise vs nibble-wise
+ * GHASH multiply) on n random cases; returns the number of mismatches. */
+int oracle_selfcheck(size_t n, uint64_t seed);
+
 #ifdef __cplusplus
 }
 #endif

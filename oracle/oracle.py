@@ -51,6 +51,9 @@ def lib():
         l.oracle_poly1305.restype = None
         l.oracle_batch.argtypes = [ctypes.c_int, ctypes.c_int, p, sz, p, p, p, p,
                                    p, p, p, p, p, p, p, sz, ctypes.c_int]
+        l.oracle_selfcheck.argtypes = [sz, ctypes.c_uint64]
+        l.oracle_ghash.argtypes = [p, p, sz, p, sz, p]
+        l.oracle_ghash.restype = None
         _lib = l
     return _lib
 
@@ -148,23 +151,45 @@ def poly1305(key, data):
     return bytearray(out.raw)
 
 
+def ghash(h, aad, ct):
+    """GHASH_H(aad, ct) incl. the length block (``AESGCM._auth`` before the
+    tag mask, aesgcm.py:60-67) for a 16-byte big-endian H."""
+    h, aad, ct = bytes(h), bytes(aad), bytes(ct)
+    out = ctypes.create_string_buffer(16)
+    lib().oracle_ghash(h, aad, len(aad), ct, len(ct), out)
+    return bytearray(out.raw)
+
+
+def selfcheck(n=20000, seed=0x5eed):
+    """Mismatches between the oracle's fast forms and the reference's own
+    formulations (``oracle_selfcheck``: T-table AES vs byte-wise rounds,
+    byte-wise vs nibble-wise GHASH multiply) over ``n`` random cases."""
+    return lib().oracle_selfcheck(n, seed)
+
+
 def _ptr(a):
     return None if a is None else a.ctypes.data_as(ctypes.c_void_p)
 
 
 def batch(alg, op, keys, nonces, aad, aad_off, aad_len, inp, in_off, inlen,
-          out_size, out_off, key_idx=None, nthreads=1):
+          out_size, out_off, key_idx=None, nthreads=1, out=None):
     """Numpy batch form (see ``oracle_batch`` in aead_oracle.h).
 
     ``alg``: "aesgcm", "chacha", "aesccm" or "aesccm8"; ``op``: "seal" or
     "open".  Returns ``(out, status)``; ``status`` is None for seal.
+    ``out``: an optional uint8 buffer of at least ``out_size`` bytes to write
+    into (reused across chunks by the whole-batch checks, so the threads do
+    not fault in fresh pages on every call).
     """
     a = {"aesgcm": 0, "chacha": 1, "aesccm": 2, "aesccm8": 3}[alg]
     o = {"seal": 0, "open": 1}[op]
     keys = np.ascontiguousarray(keys, dtype=np.uint8)
     keylen = keys.shape[-1] if keys.ndim > 1 else keys.size
     n = len(inlen)
-    out = np.zeros(out_size, dtype=np.uint8)
+    if out is None:
+        out = np.zeros(out_size, dtype=np.uint8)
+    elif out.dtype != np.uint8 or not out.flags.c_contiguous or out.size < out_size:
+        raise ValueError("out must be a contiguous uint8 buffer of >= out_size bytes")
     status = np.zeros(n, dtype=np.uint8) if o == 1 else None
     args = [np.ascontiguousarray(x) for x in (nonces, aad, inp)]
     offs = [np.ascontiguousarray(x, dtype=np.uint64) for x in (aad_off, in_off, out_off)]

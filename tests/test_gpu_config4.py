@@ -2,8 +2,10 @@
 65 536 session keys (PCG64 0x7716), 2^20 records with Zipf(1.2) lengths
 64 B-16 KiB (PCG64 0x7717), TLS 1.2 AAD seq||0x17||0x0303||len and nonce
 iv4||seq, records in arrival order (the engine's planner sorts the launch).
-Seal -> open round trip over the whole batch, and 128 sampled records
-bit-exact against the C oracle (aesgcm.py:101-124 restated)."""
+Every record's ciphertext and tag bit-exact against the threaded C oracle
+(aesgcm.py:101-124 restated; tests/fullcheck.py), the seal -> open round trip
+over the whole batch, and 128 sampled records through the oracle's
+per-record entry point."""
 import numpy as np
 import pytest
 
@@ -66,6 +68,11 @@ def _run_config4(torch, tlsgpu, oracle_mod):
             m[o:o + int(lens[i])] = True
         mt = torch.from_numpy(m).cuda()
         assert torch.equal(back[a:b][mt], inp[a:b][mt])
+    import fullcheck
+    recs, nbytes = fullcheck.check_all(torch, oracle_mod, "aesgcm", keys, inp, in_off, lens, sealed,
+                                       out_off, nonce, aad.reshape(-1), np.arange(n) * 13,
+                                       np.full(n, 13), key_idx=key_idx)
+    assert recs == n and nbytes == int(lens.sum()) + 16 * n
     pick = np.unique(np.concatenate([[0, n - 1, int(np.argmax(lens))],
                                      np.random.default_rng(4).integers(0, n, 125)]))
     for i in pick:

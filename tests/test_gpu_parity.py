@@ -186,8 +186,10 @@ def test_config1_digest(torch, tg):
 
 @pytest.mark.parametrize("alg", ["aesgcm", "chacha", "aesgcm-bs8", "chacha-regs"])
 def test_full_size_roundtrip_and_samples(torch, tg, oracle_mod, alg):
-    """2^20 x 16 KiB records: seal -> open round trip on the whole batch
-    (size-independent property), and 64 sampled records bit-exact vs the oracle.
+    """2^20 x 16 KiB records: every record's ciphertext and tag bit-exact
+    against the threaded C oracle (tests/fullcheck.py, 2^16-record chunks),
+    the seal -> open round trip on the whole batch, and 64 sampled records
+    through the oracle's per-record entry point.
     aesgcm-bs8 forces the 8-block bitsliced kernel (gcm_variant 14),
     chacha-regs the register-staged tile fill (chacha_variant 4; the default
     fills it by LDS-DMA)."""
@@ -219,6 +221,13 @@ def _full_size(torch, tg, oracle_mod, alg):
     torch.cuda.synchronize()
     assert int(status.sum()) == n
     assert torch.equal(back, inp)
+    del back
+    import fullcheck
+    recs, nbytes = fullcheck.check_all(
+        torch, oracle_mod, alg, np.frombuffer(key, np.uint8), inp, np.arange(n) * L,
+        np.full(n, L), sealed, np.arange(n) * (L + 16), fullcheck.tls13_nonces(iv, 0, n),
+        np.frombuffer(bytes(tls13_aad(L)), np.uint8), np.zeros(n), np.full(n, 5))
+    assert recs == n and nbytes == n * (L + 16)
     rng = np.random.default_rng(1)
     idx = np.unique(np.concatenate([[0, n - 1], rng.integers(0, n, 62)]))
     for i in idx:
@@ -229,5 +238,5 @@ def _full_size(torch, tg, oracle_mod, alg):
             key, nonce, pt, bytes(tls13_aad(L)))
         got = sealed[i * (L + 16):(i + 1) * (L + 16)].cpu().numpy().tobytes()
         assert got == bytes(want), i
-    del inp, back, sealed
+    del inp, sealed
     torch.cuda.empty_cache()

@@ -200,7 +200,10 @@ def test_config5_full_shape_vs_oracle(torch, tg, n):
     the hybrid octet kernel.  128 sampled wire records -- the first and the
     last among them -- equal the framing oracle's (recordlayer.py:592-641,
     :536-565 restated, pinned to the reference RecordLayer); every record
-    opens back with status ok, content type 0x17 and its fragment."""
+    opens back with status ok, content type 0x17 and its fragment.  At
+    both sizes every record's header is 17 03 03 40 11 and its ciphertext
+    and tag equal the C oracle's seal of fragment || 0x17 (tests/fullcheck.py,
+    the whole batch)."""
     import bench
     from oracle import records as R
     L = bench.C5_APP
@@ -226,6 +229,15 @@ def test_config5_full_shape_vs_oracle(torch, tg, n):
     for i, frag, w in samples:
         assert frag == orig[i].cpu().numpy().tobytes()
         assert w == R.seal_record("tls13", "aes128gcm", key, iv, seq0 + i, 0x17, frag), i
+    import fullcheck
+    from oracle import oracle as O
+    hdr = torch.tensor([0x17, 3, 3, 0x40, 0x11], dtype=torch.uint8, device="cuda")
+    assert bool((wire.view(n, WS)[:, H:H + 5] == hdr).all())
+    recs, _ = fullcheck.check_all(
+        torch, O, "aesgcm", np.frombuffer(key, np.uint8), orig.view(-1), np.arange(n) * L,
+        np.full(n, L), wire, np.arange(n) * WS + H + 5, fullcheck.tls13_nonces(iv, seq0, n),
+        hdr.cpu().numpy(), np.zeros(n), np.full(n, 5), inner_type=0x17)
+    assert recs == n
     back = torch.zeros(n * DS, dtype=torch.uint8, device="cuda")
     o_len = torch.zeros(n, dtype=torch.int32, device="cuda")
     o_ct = torch.zeros(n, dtype=torch.uint8, device="cuda")

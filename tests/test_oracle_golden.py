@@ -167,6 +167,23 @@ def test_ghash_golden_pyaead():
         assert y.to_bytes(16, "big").hex() == v["ghash"], (v["h_label"], v["aad_len"], v["ct_len"])
 
 
+def test_ghash_golden_c_oracle(oracle_mod):
+    """The C oracle's byte-wise GHASH multiply (the one its batch checks use)
+    against the reference's AESGCM._auth values for edge-case H and lengths."""
+    for v in load("ghash.json")["ghash"]:
+        aad = detbytes("ghash-aad-%d" % v["aad_len"], v["aad_len"])
+        ct = detbytes("ghash-ct-%d" % v["ct_len"], v["ct_len"])
+        got = oracle_mod.ghash(bytes.fromhex(v["h"]), aad, ct)
+        assert bytes(got).hex() == v["ghash"], (v["h_label"], v["aad_len"], v["ct_len"])
+
+
+def test_oracle_fast_forms_selfcheck(oracle_mod):
+    """T-table AES against byte-wise SubBytes/ShiftRows/MixColumns, and the
+    byte-wise GHASH multiply against the reference's nibble-wise _mul, on
+    20 000 random keys and blocks (AES-128 and AES-256 alternating)."""
+    assert oracle_mod.selfcheck(20000) == 0
+
+
 def test_poly1305_golden_extra(oracle_mod):
     """C and Python oracles against the reference's Poly1305 tags with r and s
     at their clamped maxima over long all-0xff messages."""
