@@ -500,11 +500,24 @@ int lds_attr(const void* fn, int bytes) {
     return TG_OK;
 }
 
+// tg_version()'s text; a measurement build appends its flags (common.h).
+static std::string& version_text() {
+    static std::string v = "tlsgpu 0.1.0 (gfx950)";
+    return v;
+}
+
+void note_measurement_build(const char* flag) {
+    std::string& v = version_text();
+    if (v.find("MEASUREMENT BUILD") == std::string::npos) v += " MEASUREMENT BUILD (not the product):";
+    v += " ";
+    v += flag;
+}
+
 }  // namespace tg
 
 extern "C" {
 
-const char* tg_version(void) { return "tlsgpu 0.1.0 (gfx950)"; }
+const char* tg_version(void) { return tg::version_text().c_str(); }
 
 const char* tg_last_error(void) { return g_err.c_str(); }
 

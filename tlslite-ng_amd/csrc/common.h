@@ -14,6 +14,37 @@
 
 namespace tg {
 
+// Measurement builds (tools/build_variant.sh -D...) that return wrong bytes or
+// differ from the product in their memory behaviour.  A translation unit
+// compiled with one of these flags registers itself at load time; tg_version()
+// then carries a "MEASUREMENT BUILD" marker and tlsgpu.load() refuses the
+// library unless TLSGPU_ALLOW_MEASUREMENT_BUILD=1.
+void note_measurement_build(const char* flag);
+#if defined(TG_CHACHA_NO_IO) || defined(TG_CHACHA_ILV) || defined(TG_KT_NO_GHASH) || \
+    defined(TG_KT_NO_BUILD) || defined(TG_NT_IO)
+namespace {
+struct MeasurementMark {
+    MeasurementMark() {
+#if defined(TG_CHACHA_NO_IO)
+        note_measurement_build("TG_CHACHA_NO_IO");
+#endif
+#if defined(TG_CHACHA_ILV)
+        note_measurement_build("TG_CHACHA_ILV");
+#endif
+#if defined(TG_KT_NO_GHASH)
+        note_measurement_build("TG_KT_NO_GHASH");
+#endif
+#if defined(TG_KT_NO_BUILD)
+        note_measurement_build("TG_KT_NO_BUILD");
+#endif
+#if defined(TG_NT_IO)
+        note_measurement_build("TG_NT_IO");
+#endif
+    }
+} g_measurement_mark;
+}  // namespace
+#endif
+
 // 16 tables x 256 entries x 16 bytes: M_j[b] = b * x^(8j) * H, so that
 // X * H = XOR_j M_j[byte_j(X)] (GCM bit order, aesgcm.py:8-14).
 constexpr int kGhashEntries = 16 * 256;

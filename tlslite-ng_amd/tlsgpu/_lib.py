@@ -142,6 +142,12 @@ def load():
         if name not in ("tg_version", "tg_last_error"):
             getattr(l, name).restype = ctypes.c_int
     l.tg_scan_records.restype = ctypes.c_int64
+    ver = l.tg_version().decode()
+    if "MEASUREMENT BUILD" in ver and os.environ.get("TLSGPU_ALLOW_MEASUREMENT_BUILD") != "1":
+        # a library built with a measurement-only flag (tools/build_variant.sh)
+        # may return wrong ciphertext or tags: never let it pass as the product
+        raise OSError("refusing %s: %s (set TLSGPU_ALLOW_MEASUREMENT_BUILD=1 for a measurement run)"
+                      % (path, ver))
     _lib = l
     return l
 

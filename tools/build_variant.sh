@@ -1,6 +1,9 @@
 # Build an alternative libtlsgpu.so for A/B runs (TLSGPU_LIB=...): object
 # NAME.hip recompiled with extra flags, linked with the tree's other objects.
 # usage: bash tools/build_variant.sh NAME OUT.so -DFLAG ...
+# A build with a measurement-only flag (TG_CHACHA_NO_IO, TG_CHACHA_ILV, TG_KT_NO_GHASH,
+# TG_KT_NO_BUILD, TG_NT_IO) marks tg_version() and is refused by tlsgpu.load()
+# unless TLSGPU_ALLOW_MEASUREMENT_BUILD=1 (tests/test_measurement_fence.py).
 set -e
 R=$(cd "$(dirname "$0")/.." && pwd)
 C=$R/tlslite-ng_amd/csrc
