@@ -120,6 +120,66 @@ def cpu_baseline(L, cores, seconds, gpu_samples):
             "gpu_records_rechecked": len(gpu_samples), "gpu_records_match": bool(match)}
 
 
+# ---------------------------------------------- BASELINE configs[0], in full
+
+C1_RECORDS, C1_LEN = 4096, 1024
+
+
+def _cpu_worker_c1(lo, hi, start, q):
+    """Records [lo, hi) of config 1: CHACHA20_POLY1305.seal then .open
+    (chacha20_poly1305.py:48,68) with the pure-Python restatement, TLS 1.3
+    nonce iv xor seq and AAD 17 03 03 04 10."""
+    sys.path.insert(0, ROOT)
+    from oracle import pyaead
+    from vectors import config1_inputs, tls13_aad, tls13_nonce
+    key, iv, pts = config1_inputs(C1_RECORDS, C1_LEN)
+    c = pyaead.CHACHA20_POLY1305(key)
+    start.wait()
+    t0 = time.perf_counter()
+    sealed = [bytes(c.seal(tls13_nonce(iv, s), pts[s], tls13_aad(len(pts[s])))) for s in range(lo, hi)]
+    t_seal = time.perf_counter() - t0
+    ok = all(c.open(tls13_nonce(iv, s), bytearray(w), tls13_aad(len(pts[s]))) == pts[s]
+             for s, w in zip(range(lo, hi), sealed))
+    q.put((lo, sealed, ok, t_seal, time.perf_counter() - t0))
+
+
+def cpu_config1(cores):
+    """BASELINE configs[0] run in full on the host: 4 096 x 1 KiB
+    ChaCha20-Poly1305 records sealed and opened back with oracle/pyaead.py (the
+    reference's pure-Python path restated), split over ``cores`` processes
+    started together.  The sealed stream's SHA-256 is compared with the digest
+    the reference itself produced (tests/golden/record_batch.json
+    config1.sealed_sha256)."""
+    import hashlib
+    from vectors import load
+    ctx = mp.get_context("spawn")
+    cores = max(1, min(cores, C1_RECORDS))
+    start, q = ctx.Barrier(cores + 1), ctx.Queue()
+    bounds = [(C1_RECORDS * k // cores, C1_RECORDS * (k + 1) // cores) for k in range(cores)]
+    procs = [ctx.Process(target=_cpu_worker_c1, args=(lo, hi, start, q)) for lo, hi in bounds]
+    for p in procs:
+        p.start()
+    start.wait()
+    res = sorted(q.get() for _ in procs)
+    for p in procs:
+        p.join()
+    h = hashlib.sha256()
+    for r in res:
+        for w in r[1]:
+            h.update(w)
+    want = load("record_batch.json")["config1"]["sealed_sha256"]
+    wall = max(r[4] for r in res)
+    payload = 2 * C1_RECORDS * C1_LEN
+    return {"value": round(payload / wall / 2 ** 20, 3), "unit": "MiB/s", "cores": cores,
+            "kind": "port", "records": C1_RECORDS, "record_len": C1_LEN,
+            "seconds": round(wall, 3), "seal_seconds": round(max(r[3] for r in res), 3),
+            "records_per_s": round(2 * C1_RECORDS / wall, 1),
+            "sample": "BASELINE configs[0] in full: %d x %d B ChaCha20-Poly1305 seal + open, "
+                      "oracle/pyaead.py on %d processes" % (C1_RECORDS, C1_LEN, cores),
+            "sealed_sha256": h.hexdigest(), "digest_match": h.hexdigest() == want,
+            "opened_ok": all(r[2] for r in res)}
+
+
 # -------------------------------------------------------------- GPU bench
 
 def read_bytes(n, L, op):
@@ -176,12 +236,19 @@ def main():
                          "roofline.traffic")
     ap.add_argument("--record-align", type=int, default=128,
                     help="byte alignment of each sealed record (ct||tag) in the packed batch")
-    ap.add_argument("--config", default="headline", choices=["headline", "c4", "c5", "ingest"],
-                    help="headline = BASELINE configs[1]+[2] (the metric); c4 = configs[3] "
+    ap.add_argument("--config", default="headline", choices=["headline", "c1", "c4", "c5", "ingest"],
+                    help="headline = BASELINE configs[1]+[2] (the metric); c1 = configs[0] "
+                         "(4096 x 1 KiB ChaCha20-Poly1305, the device path beside the host CPU "
+                         "run in full); c4 = configs[3] "
                          "(AES-256-GCM, 65536 keys, Zipf lengths); c5 = configs[4] (TLS 1.3 "
                          "AES-128-GCM record seal through the framing path, seq-sharded); "
                          "ingest = the host ingest pipeline (tlsgpu.ingest, SURVEY 8(f) row 3), "
                          "host memory to host memory")
+    ap.add_argument("--dist-selftest", action="store_true",
+                    help="create the process group even at world size 1 (TLSGPU_DIST_SELFTEST=1) "
+                         "so the counter reduction and the rate gather run through the backend "
+                         "(RCCL under nccl) on a one-GPU box; the line then carries dist_backend "
+                         "and dist_selftest")
     ap.add_argument("--c4-presorted", action="store_true",
                     help="config 4: pack records longest first on the host")
     ap.add_argument("--ingest-mib", type=int, default=2048,
@@ -193,7 +260,7 @@ def main():
         # N ranks, one process per GPU, started here before anything in this
         # process touches the GPU; this process only waits and passes on the
         # ranks' exit status (rank 0 prints the JSON line)
-        if args.config in ("c4", "ingest"):
+        if args.config in ("c1", "c4", "ingest"):
             ap.error("--config %s runs on one GPU (BASELINE configs[3] / the host pipeline)" % args.config)
         backend = os.environ.get("TLSGPU_DIST_BACKEND", "nccl")
         if backend == "nccl":
@@ -211,8 +278,12 @@ def main():
     if err:
         print(err, file=sys.stderr)
         sys.exit(2)
+    if args.dist_selftest:
+        os.environ["TLSGPU_DIST_SELFTEST"] = "1"
     if args.config == "ingest":
         return run_ingest(args)
+    if args.config == "c1":
+        return run_config1(args)
     if args.config == "c4":
         return run_config4(args)
     if args.config == "c5":
@@ -312,6 +383,7 @@ def main():
             "frac": round(alg_bytes / (ms / 1e3) / 1e9 / HBM_PEAK_GBS, 4),
             "frac_read": round(read_bytes(n, L, op) / (ms / 1e3) / 1e9 / HBM_PEAK_GBS, 4)}
     rows = tgd.gather_rows(torch, dist, my_ms, device=dev)
+    dist_info = tgd.selftest_collectives(torch, dist, device=dev) if tgd.group_active(dist) else None
     dom = max(per_kernel, key=lambda k: per_kernel[k]["ms"])
     dom_op = "open" if dom.endswith("open") else "seal"
     dom_s = per_kernel[dom]["ms"] / 1e3
@@ -355,7 +427,10 @@ def main():
             "verified_per_cipher": verified,
             "auth_failures": int(sums[2]),
             "auth_failures_per_cipher": fails,
+            "dist_backend": dist.get_backend() if tgd.group_active(dist) else None,
         }
+        if dist_info:
+            line["dist_selftest"] = dist_info
         if world > 1:
             names = ["%s_%s" % k for k in kinds]
             line["per_rank"] = [{nm: {"ms": round(ms, 3),
@@ -367,8 +442,9 @@ def main():
         if not args.no_cpu_baseline and world == 1:
             cores = args.cpu_cores or host_cores()[0]
             line["cpu_baseline"] = cpu_baseline(L, cores, args.cpu_seconds, samples)
+            line["cpu_baseline"]["config1"] = cpu_config1(cores)
         print(json.dumps(line), flush=True)
-    if world > 1:
+    if tgd.group_active(dist):
         dist.destroy_process_group()
     if not ok:
         sys.exit(3)
@@ -536,6 +612,62 @@ def cpu_baseline_c5(L, cores, seconds):
                       "of the reference path)" % (cores, seconds, L)}
 
 
+def run_config1(args):
+    """BASELINE configs[0] (ChaCha20-Poly1305 seal + open of 4 096 x 1 KiB
+    records, chacha20_poly1305.py:48,68): the device batch path, timed per
+    step with HIP events on the launch stream, its sealed stream checked
+    against the reference's digest (record_batch.json config1.sealed_sha256)
+    and every record opened back; beside it the same workload run in full on
+    the host cores with the pure-Python restatement (cpu_config1)."""
+    import hashlib
+    import numpy as np
+    import torch
+    import tlsgpu
+    from vectors import config1_inputs, load, tls13_aad
+    key, iv, pts = config1_inputs(C1_RECORDS, C1_LEN)
+    n, L = C1_RECORDS, C1_LEN
+    inp = torch.from_numpy(np.frombuffer(b"".join(bytes(p) for p in pts), np.uint8).copy()).cuda()
+    out = torch.zeros(n * (L + TAG_LEN), dtype=torch.uint8, device="cuda")
+    back = torch.zeros_like(inp)
+    status = torch.zeros(n, dtype=torch.uint8, device="cuda")
+    nonces = torch.zeros(NONCE_LEN * n, dtype=torch.uint8, device="cuda")
+    tlsgpu.make_nonces(iv, 0, n, nonces)
+    aad = torch.from_numpy(np.frombuffer(bytes(tls13_aad(L)), np.uint8).copy()).cuda()
+    c = tlsgpu.HipCHACHA20_POLY1305(key)
+    sb = tlsgpu.make_batch(n, inp, out, nonces, aad=aad, fixed_len=L, in_stride=L,
+                           out_stride=L + TAG_LEN, fixed_aad_len=AAD_LEN)
+    ob = tlsgpu.make_batch(n, out, back, nonces, aad=aad, fixed_len=L, in_stride=L + TAG_LEN,
+                           out_stride=L, fixed_aad_len=AAD_LEN, status=status)
+    stream = torch.cuda.current_stream()
+    evs = []
+    for k in range(args.warmup + args.steps):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        tlsgpu.seal_batch(c, sb, stream)
+        tlsgpu.open_batch(c, ob, stream)
+        e1.record(stream)
+        if k >= args.warmup:
+            evs.append((e0, e1))
+    torch.cuda.synchronize()
+    ms = sum(a.elapsed_time(b) for a, b in evs) / len(evs)
+    digest = hashlib.sha256(out.cpu().numpy().tobytes()).hexdigest()
+    want = load("record_batch.json")["config1"]["sealed_sha256"]
+    ok = digest == want and int(status.sum()) == n and bool(torch.equal(back, inp))
+    line = {"metric": "MiB/s ChaCha20-Poly1305 seal+open, 4096 x 1 KiB (BASELINE configs[0])",
+            "value": round(2 * n * L / (ms / 1e3) / 2 ** 20, 1), "unit": "MiB/s", "n_gpus": 1,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms, 4),
+            "higher_is_better": True, "scaling": "none", "dtype": "u8",
+            "data": "config1_inputs(): random.Random(0) key, iv and plaintexts",
+            "config": {"workload": "configs[0]: 4096 x 1 KiB ChaCha20-Poly1305 seal + open, "
+                                   "TLS 1.3 nonce and AAD", "records": n, "record_len": L},
+            "sealed_sha256": digest, "digest_match": digest == want, "verified": bool(ok)}
+    if not args.no_cpu_baseline:
+        line["cpu_baseline"] = cpu_config1(args.cpu_cores or host_cores()[0])
+    print(json.dumps(line), flush=True)
+    if not ok:
+        sys.exit(3)
+
+
 def run_config5(args):
     """BASELINE configs[4]: TLS 1.3 AES-128-GCM record seal, 2^20 records per
     GPU of L = 16384 application bytes through the device framing path
@@ -604,6 +736,7 @@ def run_config5(args):
     ok = ok and hdr == bytes([0x17, 0x03, 0x03, (L + 17) >> 8, (L + 17) & 0xff])
     sums, elapsed = tgd.reduce_counters(torch, dist, [n * args.steps, n * L * args.steps, 0],
                                         elapsed, device="cuda")
+    dist_info = tgd.selftest_collectives(torch, dist, device="cuda") if tgd.group_active(dist) else None
     ms = sum(a.elapsed_time(b) for a, b in evs) / len(evs)
     ach = c5_algorithmic_bytes(n, L, "seal") / (ms / 1e3) / 1e9
     if rank == 0:
@@ -626,7 +759,10 @@ def run_config5(args):
                          "bytes_per_record": c5_algorithmic_bytes(1, L, "seal"), "traffic": None,
                          "ms": round(ms, 3)},
             "oracle_checked_records": len(samples), "oracle_mismatches": bad,
-            "verified": bool(ok)}
+            "verified": bool(ok),
+            "dist_backend": dist.get_backend() if tgd.group_active(dist) else None}
+        if dist_info:
+            line["dist_selftest"] = dist_info
         tr = c5_traffic(args.traffic_file, n, L) if world == 1 else None
         if tr:
             line["roofline"]["traffic"] = tr["hbm_bytes"]
@@ -635,7 +771,7 @@ def run_config5(args):
             cores = args.cpu_cores or host_cores()[0]
             line["cpu_baseline"] = cpu_baseline_c5(L, cores, args.cpu_seconds)
         print(json.dumps(line), flush=True)
-    if world > 1:
+    if tgd.group_active(dist):
         dist.destroy_process_group()
     if not ok:
         sys.exit(3)

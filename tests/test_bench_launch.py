@@ -71,3 +71,13 @@ def test_nccl_needs_a_gpu_per_rank():
 def test_single_gpu_configs_refuse_n(config):
     r = _run(["--gpus", "2", "--config", config])
     assert r.returncode == 2 and "runs on one GPU" in r.stderr
+
+
+def test_cpu_config1_in_full_matches_reference_digest():
+    """bench.py's config-1 CPU leg (BASELINE configs[0] in full, 4 096 x 1 KiB
+    ChaCha20-Poly1305 with the pure-Python restatement, split over processes):
+    the sealed stream equals the reference's own digest and opens back."""
+    import bench
+    r = bench.cpu_config1(4)
+    assert r["digest_match"] and r["opened_ok"] and r["cores"] == 4 and r["records"] == 4096
+    assert r["value"] > 0

@@ -102,6 +102,7 @@ def _worker(rank, world, port, outdir):
     elapsed = tgd.timed(torch, dist, world, step, STEPS)
     sums, tmax = tgd.reduce_counters(torch, dist, [count * STEPS, count * LEN * STEPS, 0], elapsed)
     rows = tgd.gather_rows(torch, dist, [rank, count, first])
+    assert tgd.selftest_collectives(torch, dist)["ok"]
     with open(os.path.join(outdir, "rank%d" % rank), "w") as f:
         f.write("%d %d %d %.6f %.6f\n" % (sums[0], sums[1], sums[2], tmax, elapsed))
         f.write(repr(rows) + "\n")
@@ -137,3 +138,27 @@ def test_world2_sharded_seal_equals_single(tmp_path):
     for s in range(total):
         want = oracle.chacha_seal(KEY, tls13_nonce(IV, s), _pt(s), tls13_aad(LEN))
         assert open(tmp_path / ("rec%05d" % s), "rb").read() == bytes(want)
+
+
+def _world1_worker(_, outdir):
+    for k in ("MASTER_ADDR", "MASTER_PORT", "WORLD_SIZE", "RANK", "LOCAL_RANK"):
+        os.environ.pop(k, None)
+    os.environ["TLSGPU_DIST_SELFTEST"] = "1"
+    w, r, _, dev = tgd.init_process(torch, dist, backend="gloo", use_gpu=False)
+    assert (w, r, dev) == (1, 0, None) and tgd.group_active(dist)
+    info = tgd.selftest_collectives(torch, dist)
+    sums, tmax = tgd.reduce_counters(torch, dist, [3, 4, 0], 1.5)
+    rows = tgd.gather_rows(torch, dist, [7.0, 8.0])
+    dist.destroy_process_group()
+    with open(os.path.join(outdir, "world1"), "w") as f:
+        f.write(repr((info["ok"], info["backend"], info["world"], sums, tmax, rows)))
+
+
+def test_world1_group_selftest(tmp_path):
+    """bench.py --dist-selftest at world size 1: the group is created anyway
+    (tcp rendezvous on 127.0.0.1 outside torch.distributed.run) and the
+    counter reduction, rate gather and collective self-test go through the
+    backend (gloo here; RCCL in the -m gpu test)."""
+    mp.spawn(_world1_worker, args=(str(tmp_path),), nprocs=1, join=True)
+    got = eval(open(tmp_path / "world1").read())   # noqa: S307 -- our own repr
+    assert got == (True, "gloo", 1, [3.0, 4.0, 0.0], 1.5, [[7.0, 8.0]])

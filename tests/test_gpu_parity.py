@@ -180,6 +180,14 @@ def test_config1_digest(torch, tg):
     torch.cuda.synchronize()
     assert hashlib.sha256(out.cpu().numpy().tobytes()).hexdigest() == \
         BATCH["config1"]["sealed_sha256"]
+    # and the whole batch opens back to the plaintexts (chacha20_poly1305.py:68)
+    back = torch.zeros_like(inp)
+    status = torch.zeros(n, dtype=torch.uint8, device="cuda")
+    tg.open_batch(obj, tg.make_batch(n, out, back, nonces, aad=aad, fixed_len=1024,
+                                     in_stride=1040, out_stride=1024, aad_stride=0,
+                                     fixed_aad_len=5, status=status))
+    torch.cuda.synchronize()
+    assert int(status.sum()) == n and torch.equal(back, inp)
 
 
 # ------------------------------------------- full-size (BASELINE configs 2/3)

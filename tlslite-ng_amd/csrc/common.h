@@ -9,6 +9,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <atomic>
+
 #include "keymath.h"
 #include "tlsgpu.h"
 
@@ -268,17 +270,22 @@ int lds_attr(const void* fn, int bytes);
 // Compute units of the current device (grid size of the persistent kernels),
 // looked up once per device.
 inline int device_cus() {
-    static int cache[64] = {0};
+    // one entry per device, filled by whichever thread gets there first;
+    // every thread would store the same value, but the entries are atomics so
+    // concurrent tg_seal / tg_open calls on one handle are race-free
+    static std::atomic<int> cache[64];
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) dev = 0;
-    if (!cache[dev]) {
+    int v = cache[dev].load(std::memory_order_relaxed);
+    if (!v) {
         int cus = 0;
         if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
             cus <= 0)
             cus = 256;
-        cache[dev] = cus;
+        cache[dev].store(cus, std::memory_order_relaxed);
+        v = cus;
     }
-    return cache[dev];
+    return v;
 }
 
 }  // namespace tg

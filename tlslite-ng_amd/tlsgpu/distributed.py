@@ -26,15 +26,30 @@ def env_rank():
             int(os.environ.get("LOCAL_RANK", "0")))
 
 
-def init_process(torch, dist, backend=None, use_gpu=True):
+def _free_port():
+    import socket
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        return so.getsockname()[1]
+
+
+def init_process(torch, dist, backend=None, use_gpu=True, group_at_world1=None):
     """One process per GPU.  backend None = TLSGPU_DIST_BACKEND or "nccl"
     (= RCCL over xGMI on ROCm).  Under nccl every rank needs its own device:
     LOCAL_RANK >= device count is an error (no silent oversubscription).  gloo
     is the CPU rehearsal backend; with use_gpu it may map several ranks to one
     device (rank % device count), which is only for rehearsals.
+
+    A process group is created for world > 1, and also at world 1 when
+    ``group_at_world1`` (default: TLSGPU_DIST_SELFTEST=1) asks for it, so the
+    collectives below run through the backend on a one-GPU box too (the RCCL
+    self-test, bench.py --dist-selftest).  Outside torch.distributed.run the
+    rendezvous is tcp://127.0.0.1 on a free port.
     Returns (world, rank, local_rank, device or None)."""
     world, rank, local = env_rank()
     backend = backend or os.environ.get("TLSGPU_DIST_BACKEND", "nccl")
+    if group_at_world1 is None:
+        group_at_world1 = os.environ.get("TLSGPU_DIST_SELFTEST") == "1"
     device = None
     if use_gpu:
         ndev = torch.cuda.device_count()
@@ -45,12 +60,48 @@ def init_process(torch, dist, backend=None, use_gpu=True):
                             "per local rank" % (local, ndev))
         device = local if backend == "nccl" else local % ndev
         torch.cuda.set_device(device)
-    if world > 1:
+    elif backend == "nccl":
+        raise DistError("the nccl backend needs a GPU per rank")
+    if world > 1 or group_at_world1:
+        kw = {}
+        if "MASTER_ADDR" not in os.environ:
+            kw = {"init_method": "tcp://127.0.0.1:%d" % _free_port(), "world_size": world,
+                  "rank": rank}
         if backend == "nccl":
-            dist.init_process_group("nccl", device_id=torch.device("cuda", device))
+            dist.init_process_group("nccl", device_id=torch.device("cuda", device), **kw)
         else:
-            dist.init_process_group(backend)
+            dist.init_process_group(backend, **kw)
     return world, rank, local, device
+
+
+def group_active(dist):
+    """True when a process group exists (world > 1, or the world-1 self-test):
+    the collectives below then go through the backend."""
+    return dist.is_available() and dist.is_initialized()
+
+
+def selftest_collectives(torch, dist, device=None):
+    """The collectives bench.py uses, checked on known values: an all_reduce
+    SUM and MAX of rank-dependent tensors and an all_gather of a per-rank row.
+    Returns a dict for the bench line; ``ok`` is False on any mismatch."""
+    if not group_active(dist):
+        raise DistError("no process group")
+    world, rank = dist.get_world_size(), dist.get_rank()
+    c = torch.tensor([1.0, float(rank), 2.0 ** 40 + rank], dtype=torch.float64, device=device)
+    dist.all_reduce(c, op=dist.ReduceOp.SUM)
+    t = torch.tensor([float(rank) * 3.0], dtype=torch.float64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    row = torch.tensor([float(rank), float(rank) + 0.5], dtype=torch.float64, device=device)
+    rows = [torch.zeros_like(row) for _ in range(world)]
+    dist.all_gather(rows, row)
+    if device is not None:
+        torch.cuda.synchronize()
+    want_sum = [float(world), float(world * (world - 1) // 2),
+                world * 2.0 ** 40 + world * (world - 1) // 2]
+    ok = (c.tolist() == want_sum and t.item() == 3.0 * (world - 1) and
+          [r.tolist() for r in rows] == [[float(g), g + 0.5] for g in range(world)])
+    return {"backend": dist.get_backend(), "world": world, "all_reduce_sum": c.tolist(),
+            "all_reduce_max": t.item(), "all_gather_rows": world, "ok": bool(ok)}
 
 
 def shard_range(n_total, world, rank):
@@ -95,7 +146,7 @@ def _sync(torch):
 def barrier(torch, dist, world):
     """Device sync, then (N > 1) a process barrier, then device sync."""
     _sync(torch)
-    if world > 1:
+    if group_active(dist):
         dist.barrier()
     _sync(torch)
 
@@ -116,7 +167,7 @@ def reduce_counters(torch, dist, counters, elapsed, device=None):
     all ranks.  Returns (summed list, max elapsed)."""
     c = torch.tensor([float(x) for x in counters], dtype=torch.float64, device=device)
     t = torch.tensor([float(elapsed)], dtype=torch.float64, device=device)
-    if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+    if group_active(dist):
         dist.all_reduce(c, op=dist.ReduceOp.SUM)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return [float(x) for x in c.tolist()], float(t.item())
@@ -126,7 +177,7 @@ def gather_rows(torch, dist, row, device=None):
     """All ranks' ``row`` (list of numbers, same length everywhere) as a list
     of lists indexed by rank (the per-rank kernel rates of the report)."""
     t = torch.tensor([float(x) for x in row], dtype=torch.float64, device=device)
-    if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+    if group_active(dist):
         out = [torch.zeros_like(t) for _ in range(dist.get_world_size())]
         dist.all_gather(out, t)
         return [[float(x) for x in o.tolist()] for o in out]
