@@ -78,7 +78,9 @@ int tg_init(int device);                   /* hipSetDevice for the calling threa
  *   no_plan            1 = no length-sorted launch order
  *   stage_copy         1 = per-record calls copy through device memory
  *   hy_t, hy_prio      hybrid AES-GCM kernel: T-table waves (0 = auto: 10
- *                      of 16, -1 = none), 1 = T-table waves at raised priority
+ *                      of 16, -1 = none; more than the workgroup's waves
+ *                      fails the launch with TG_EINVAL), 1 = T-table waves
+ *                      at raised priority
  *   hy_threads         hybrid AES-GCM workgroup: 0 = 1024, or 768
  * An unknown name is TG_EINVAL; a variant a launcher does not know makes
  * its launches fail with TG_EINVAL. */
@@ -124,7 +126,8 @@ int tg_open(tg_key* k, const uint8_t* nonce, size_t noncelen,
  *            aad_len ? aad_len[i] : fixed_aad_len bytes
  *   key      key table entry key_idx ? key_idx[i] : 0; key_idx[i] must be
  *            below the table's nkeys -- a record with an index out of range
- *            is skipped (never read past the table; open: status[i] = 0)
+ *            is skipped (never read past the table; open: status[i] = 0
+ *            and its plaintext output zeroed, as a rejected record's)
  *   status   open only: status[i] = 1 authentic / 0 rejected (pt zeroed)
  * len == NULL means every record is fixed_len bytes.  Offsets with 16-byte
  * alignment take the vector path; any alignment is accepted.

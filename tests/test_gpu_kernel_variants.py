@@ -218,7 +218,9 @@ def test_key_table_octet_kernel(torch, tg, oracle_mod, klen, keys, align, varian
 def test_key_index_out_of_range_is_skipped(torch, tg, oracle_mod, alg, opts):
     """A key-table record whose key_idx is not below the table's size is
     never read past the table: seal leaves its output alone, open reports
-    status 0; every other record is sealed and opened as usual."""
+    status 0 and zeroes its plaintext output (as a rejected record's; the
+    output buffer starts filled with 0xaa); every other record is sealed and
+    opened as usual."""
     from batchpack import HostBatch
     nk = 7
     rng = np.random.default_rng(55)
@@ -249,7 +251,7 @@ def test_key_index_out_of_range_is_skipped(torch, tg, oracle_mod, alg, opts):
             assert not got[o:o + L + 16].any(), ("skipped record written", i)
         # open: the good records' sealed bytes back, bad ones rejected
         src = d["out"].clone()
-        pt = torch.zeros(hb.in_bytes, dtype=torch.uint8, device="cuda")
+        pt = torch.full((hb.in_bytes,), 0xaa, dtype=torch.uint8, device="cuda")
         status = torch.full((hb.n,), 7, dtype=torch.uint8, device="cuda")
         tg.open_batch(table, tg.make_batch(hb.n, src, pt, d["nonces"], aad=d["aad"], lens=d["lens"],
                                            in_off=d["out_off"], out_off=d["in_off"], aad_off=d["aad_off"],
@@ -259,6 +261,26 @@ def test_key_index_out_of_range_is_skipped(torch, tg, oracle_mod, alg, opts):
         assert (st[bad] == 0).all()
         assert (st[good] == 1).all()
         back = pt.cpu().numpy()
+        for i in bad:
+            o, L = int(hb.in_off[i]), int(hb.lens[i])
+            assert not back[o:o + L].any(), ("skipped record's plaintext not zeroed", i)
         for i in good[::37]:
             o, L = int(hb.in_off[i]), int(hb.lens[i])
             assert np.array_equal(back[o:o + L], hb.inp[o:o + L]), ("open", i)
+
+
+def test_hy_t_out_of_range_fails_launch(torch, tg):
+    """hy_t above the hybrid workgroup's waves is TG_EINVAL at launch (no
+    silent fallback to the default split); hy_t within range works."""
+    n, L = 32768, 16    # above the wave kernel's limit: the hybrid kernel
+    inp = torch.zeros(n * L, dtype=torch.uint8, device="cuda")
+    out = torch.zeros(n * (L + 16), dtype=torch.uint8, device="cuda")
+    nonces = torch.zeros(12 * n, dtype=torch.uint8, device="cuda")
+    key = tg.HipAESGCM(bytearray(16))
+    b = tg.make_batch(n, inp, out, nonces, fixed_len=L, in_stride=L, out_stride=L + 16)
+    with tg.options(gcm_variant=15, hy_t=17):
+        with pytest.raises(tg.TlsGpuError):
+            tg.seal_batch(key, b)
+    with tg.options(gcm_variant=15, hy_t=16):
+        tg.seal_batch(key, b)
+    torch.cuda.synchronize()

@@ -116,6 +116,35 @@ struct KeyPlanesVmem {
 // they measured no better).
 struct KeyPlanesVmemFolded : KeyPlanesVmem {
     static constexpr bool kFolded = true;
+    static constexpr bool kRound = false;
+};
+
+// The folded rows by VECTOR loads: the address carries the lane's opaque zero
+// ``zv``, so the compiler cannot scalarise it and the words arrive in VGPRs.
+// As SGPR operands the 32 T gates of every round issue at half rate (any VALU
+// instruction that reads an SGPR does on gfx950, profiles/r04/probe4.txt).
+// encrypt() fetches a whole round's eight rows (32 VGPRs) at the start of the
+// round, so the S-box gates hide the load latency; the vector-memory path is
+// otherwise idle in the octet kernels.
+struct KeyPlanesVec {
+    static constexpr bool kFolded = true;
+    static constexpr bool kRound = true;
+    const uint4* rows;
+    uint32_t zv;
+    TG_BS_MF void round(int r, Word4 (&c)[8]) const {
+#if defined(__HIP_DEVICE_COMPILE__)
+        typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+        const uint8_t* base = reinterpret_cast<const uint8_t*>(rows + 8 * r) + zv;
+#pragma unroll
+        for (int b = 0; b < 8; ++b) {
+            const v4u v = *(const __attribute__((address_space(1))) v4u*)(base + 16 * b);
+            c[b] = make_uint4(v.x, v.y, v.z, v.w);
+        }
+#else
+        for (int b = 0; b < 8; ++b) c[b] = rows[8 * r + b];
+#endif
+    }
+    TG_BS_MF Word4 row4(int r, int b) const { return rows[8 * r + b]; }
 };
 
 // Plane (r, i, b) of the (NR + 1) * 32 in ``src`` (GcmKeyDev::bs8mask order)
@@ -263,6 +292,42 @@ TG_BS_HD void mix_round_folded(uint32_t (*s)[8], const KM& km, int r) {
     }
 }
 
+// mix_round_folded from a round's rows already in registers (KeyPlanesVec).
+TG_BS_HD void mix_round_rows(uint32_t (*s)[8], const Word4 (&c)[8]) {
+    uint32_t a7[4], T7[4], Tp[4];
+    const uint32_t c7w[4] = {c[7].x, c[7].y, c[7].z, c[7].w};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) a7[i] = rotr_bytes(s[i][7], i);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) T7[i] = xor3(a7[i], a7[(i + 1) & 3], c7w[i]);
+    TG_BS8_FENCE();
+#pragma unroll
+    for (int b = 0; b < 8; ++b) {
+        uint32_t a[4], T[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) a[i] = b == 7 ? a7[i] : rotr_bytes(s[i][b], i);
+        if (b == 7) {
+#pragma unroll
+            for (int i = 0; i < 4; ++i) T[i] = T7[i];
+        } else {
+            const uint32_t cw[4] = {c[b].x, c[b].y, c[b].z, c[b].w};
+#pragma unroll
+            for (int i = 0; i < 4; ++i) T[i] = xor3(a[i], a[(i + 1) & 3], cw[i]);
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const uint32_t Tprev = b == 0 ? T7[i] : Tp[i];
+            if (b == 1 || b == 3 || b == 4)
+                s[i][b] = xor3(Tprev, T7[i], a[(i + 1) & 3]) ^ T[(i + 2) & 3];
+            else
+                s[i][b] = xor3(Tprev, a[(i + 1) & 3], T[(i + 2) & 3]);
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) Tp[i] = T[i];
+        TG_BS8_FENCE();
+    }
+}
+
 // 8 x 8 bit transpose inside every byte of a[0..7]: bit j of byte c of a[b]
 // <-> bit b of byte c of a[j] (three swap stages, two shifts + two bitop3
 // per pair).
@@ -341,8 +406,22 @@ TG_BS_HD void to_blocks(uint32_t (*x)[8], uint32_t (*w)[8]) {
 // caller computes their S-box once per record (rows 2 and 3 carry counter
 // bytes 14 and 15): two of the four S-box calls of round 1 (144 of ~4 500
 // instructions per batch of eight blocks).
+template <class KM, class = void>
+struct RoundRows {
+    static constexpr bool value = false;
+};
+template <class KM>
+struct RoundRows<KM, decltype((void)KM::kRound)> {
+    static constexpr bool value = KM::kRound;
+};
+template <class KM>
+TG_BS_HD constexpr bool round_rows() { return RoundRows<KM>::value; }
+
 template <int NR, class KM>
 TG_BS_HD void encrypt(uint32_t (*s)[8], const KM& km, uint32_t (*w)[8], bool sub01 = true) {
+    // KeyPlanesVec: the round's key rows are fetched before its S-box gates
+    Word4 c[8];
+    if constexpr (round_rows<KM>()) km.round(1, c);
     // round 1 peeled off the rolled loop: its S-box of rows 0-1 is optional
     if (sub01) {
         bs::sbox(s[0]);
@@ -354,7 +433,9 @@ TG_BS_HD void encrypt(uint32_t (*s)[8], const KM& km, uint32_t (*w)[8], bool sub
     TG_BS8_FENCE();
     bs::sbox(s[3]);
     TG_BS8_FENCE();
-    if constexpr (KM::kFolded)
+    if constexpr (round_rows<KM>())
+        mix_round_rows(s, c);
+    else if constexpr (KM::kFolded)
         mix_round_folded(s, km, 1);
     else
         mix_round(s, km, 1);
@@ -362,12 +443,15 @@ TG_BS_HD void encrypt(uint32_t (*s)[8], const KM& km, uint32_t (*w)[8], bool sub
 #pragma unroll 1
 #endif
     for (int r = 2; r < NR; ++r) {
+        if constexpr (round_rows<KM>()) km.round(r, c);
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
             bs::sbox(s[i]);
             TG_BS8_FENCE();
         }
-        if constexpr (KM::kFolded)
+        if constexpr (round_rows<KM>())
+            mix_round_rows(s, c);
+        else if constexpr (KM::kFolded)
             mix_round_folded(s, km, r);
         else
             mix_round(s, km, r);

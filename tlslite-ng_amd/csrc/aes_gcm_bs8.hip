@@ -509,6 +509,8 @@ __global__ __launch_bounds__(THREADS) void gcm_hy_kernel(const GcmKeyDev* __rest
         }
     } else {
         const RkLds none{0};
+        uint32_t zv = 0;   // the key rows' vector loads (bs8::KeyPlanesVec)
+        asm volatile("v_mov_b32 %0, 0" : "=v"(zv));
         for (;;) {
             uint32_t job = 0;
             if ((threadIdx.x & 63u) == 0) job = atomicAdd(queue, 1u);
@@ -516,9 +518,9 @@ __global__ __launch_bounds__(THREADS) void gcm_hy_kernel(const GcmKeyDev* __rest
             if (job >= njobs) break;
             asm volatile("" ::: "memory");
             const tg_batch b = *bp;
-            octet_job<NR, OPEN, false, bs8::KeyPlanesVmemFolded, SingleKeyRowCtx, (THREADS < 1024)>(
+            octet_job<NR, OPEN, false, bs8::KeyPlanesVec, SingleKeyRowCtx, (THREADS < 1024)>(
                 SingleKeyRowCtx{key, jw}, b, order, 8ull * job, recw, none, kHySbox,
-                bs8::KeyPlanesVmemFolded{{krows}});
+                bs8::KeyPlanesVec{krows, zv});
         }
     }
 }
@@ -564,6 +566,7 @@ int launch_hy(const GcmKeyDev* key, const tg_batch& b, hipStream_t s, const uint
     const int t = opt(kOptHyT);
     const bool small = opt(kOptHyThreads) == 768;
     const int waves = small ? 12 : 16;
+    if (t > waves) return TG_EINVAL;   // more T-table waves than the workgroup has
     // t < 0: bitsliced waves only (measurement)
     const uint32_t nt = t < 0 ? 0u : t > 0 && t <= waves ? (uint32_t)t : small ? 6u : 10u;
     const uint32_t prio = opt(kOptHyPrio) == 1 ? 1u : 0u;

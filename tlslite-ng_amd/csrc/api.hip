@@ -104,35 +104,51 @@ void free_stage(Stage* st) {
     delete st;
 }
 
-// A free staging slot of this key (a new one if all are in use); NULL on error.
-Stage* take_stage(tg_key* k) {
+// A free staging slot of this key (a new one if all are in use).  Returns
+// TG_OK with *out set, or the error code recorded by fail() (TG_ENOMEM for
+// host memory, TG_EHIP when the stream cannot be created).
+int take_stage(tg_key* k, Stage** out) {
     {
         std::lock_guard<std::mutex> g(k->stage_mu);
         if (!k->free_stages.empty()) {
-            Stage* st = k->free_stages.back();
+            *out = k->free_stages.back();
             k->free_stages.pop_back();
-            return st;
+            return TG_OK;
         }
     }
     Stage* st = new (std::nothrow) Stage();
-    if (!st) {
-        fail(TG_ENOMEM, "out of host memory");
-        return nullptr;
-    }
+    if (!st) return fail(TG_ENOMEM, "out of host memory");
     hipError_t e = hipStreamCreateWithFlags(&st->stream, hipStreamNonBlocking);
     if (e != hipSuccess) {
         delete st;
-        fail(TG_EHIP, "hipStreamCreate: %s", hipGetErrorString(e));
-        return nullptr;
+        return fail(TG_EHIP, "hipStreamCreate: %s", hipGetErrorString(e));
     }
     std::lock_guard<std::mutex> g(k->stage_mu);
     k->stages.push_back(st);
-    return st;
+    *out = st;
+    return TG_OK;
 }
 
+// Idle slots a key keeps; a slot given back beyond these is freed, so a burst
+// of concurrent calls does not pin its buffers for the key's lifetime.
+constexpr size_t kMaxIdleStages = 4;
+
 void give_stage(tg_key* k, Stage* st) {
-    std::lock_guard<std::mutex> g(k->stage_mu);
-    k->free_stages.push_back(st);
+    {
+        std::lock_guard<std::mutex> g(k->stage_mu);
+        if (k->free_stages.size() < kMaxIdleStages) {
+            k->free_stages.push_back(st);
+            return;
+        }
+        for (size_t i = 0; i < k->stages.size(); ++i)
+            if (k->stages[i] == st) {
+                k->stages[i] = k->stages.back();
+                k->stages.pop_back();
+                break;
+            }
+    }
+    (void)hipStreamSynchronize(st->stream);
+    free_stage(st);
 }
 
 int ensure_stage(Stage* st, size_t bytes) {
@@ -320,8 +336,8 @@ int single(tg_key* k, const uint8_t* nonce, size_t noncelen, const uint8_t* aad,
     const size_t o_st = align16(o_out + outlen), total = o_st + 16;
     int rc = select_device(k);
     if (rc) return rc;
-    Stage* st = take_stage(k);
-    if (!st) return TG_ENOMEM;
+    Stage* st = nullptr;
+    if ((rc = take_stage(k, &st))) return rc;
     rc = single_staged(k, st, nonce, aad, aadlen, in, inlen, out, open, len, outlen, o_aad, o_in, o_out,
                        o_st, total);
     give_stage(k, st);
@@ -340,6 +356,8 @@ int batch(tg_key* k, const tg_batch* b, void* stream, bool open) {
     hipStream_t s = static_cast<hipStream_t>(stream);  // NULL = the null stream
     if ((rc = launch(k, *b, open, s))) return fail(rc, "kernel launch failed: %s",
                                                    hipGetErrorString(hipGetLastError()));
+    if (open && k->nkeys > 1 && (rc = tg_launch_zero_skipped(*b, k->nkeys, s)))
+        return fail(rc, "zeroing skipped records failed");
     return TG_OK;
 }
 

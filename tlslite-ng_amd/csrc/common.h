@@ -305,6 +305,9 @@ int tg_launch_gcm_bs8(const tg::GcmKeyDev* key, int rounds, const tg_batch& b, b
 int tg_launch_table_hpow(const tg::GcmTableKey* keys, uint64_t n, uint4* hpow, hipStream_t s);
 int tg_length_order(const uint32_t* len, uint64_t n, uint32_t* order, void* scratch, size_t* bytes,
                     hipStream_t s);
+// Open over a key table: zero the output of every record whose key_idx is not
+// below nkeys (the AEAD kernels skip it with status 0; planner.hip).
+int tg_launch_zero_skipped(const tg_batch& b, uint64_t nkeys, hipStream_t s);
 // Key-grouped jobs of a key-table batch (planner.hip): records of at least
 // ``split`` bytes with key_idx < nkeys in front, grouped by key and cut into
 // jobs of at most jobsz (a power of two) records of one key; the rest

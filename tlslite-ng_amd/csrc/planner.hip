@@ -37,6 +37,31 @@ int tg_length_order(const uint32_t* len, uint64_t n, uint32_t* order, void* scra
     return TG_OK;
 }
 
+// ---- open over a key table: records with an out-of-range key_idx ---------
+// The AEAD kernels skip such a record (status 0, never reading past the
+// table); this pass zeroes its plaintext output over len[i] bytes, as for a
+// rejected record (include/tlsgpu.h: a status-0 record's plaintext is zero).
+// One thread per record; the common case (every index in range) reads the
+// key index and exits.
+namespace {
+__global__ void zero_skipped_kernel(tg_batch b, uint64_t nkeys) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= b.n || b.key_idx[i] < nkeys) return;
+    uint8_t* o = tg::rec_out(b, i);
+    const uint32_t L = tg::rec_len(b, i);
+    uint32_t k = 0;
+    for (; k < L && (((uintptr_t)(o + k)) & 3u); ++k) o[k] = 0;
+    for (; k + 4 <= L; k += 4) *reinterpret_cast<uint32_t*>(o + k) = 0u;
+    for (; k < L; ++k) o[k] = 0;
+}
+}  // namespace
+
+int tg_launch_zero_skipped(const tg_batch& b, uint64_t nkeys, hipStream_t s) {
+    if (b.n == 0 || !b.key_idx) return TG_OK;
+    hipLaunchKernelGGL(zero_skipped_kernel, dim3((unsigned)((b.n + 255) / 256)), dim3(256), 0, s, b, nkeys);
+    return hipGetLastError() == hipSuccess ? TG_OK : TG_EHIP;
+}
+
 // ---- key-grouped octet jobs (key-table AES-GCM, aes_gcm_bs8.hip) ---------
 // The records of a key-table batch sorted by (key, length descending), then
 // cut into jobs of at most eight consecutive records of one key, so that a
