@@ -70,6 +70,10 @@ int tg_init(int device);                   /* hipSetDevice for the calling threa
  *   kt_lpr             key-table long records: lanes per record of the
  *                      key-grouped bitsliced kernel (8 / 16 / 32 / 64; 0 =
  *                      32), -1 = the wave-per-record T-table kernel
+ *   kt_hybrid, kt_t    key-table long records at 32 lanes per record: 0 =
+ *                      the persistent T-table + bitsliced kernel, -1 = the
+ *                      bitsliced key-grouped kernel; its T-table waves (0 =
+ *                      7 of 11, at most 11)
  *   chacha_variant     0 auto, 3 wave per record, 4 lane per record with
  *                      the register-staged tile, 5 lane per record with the
  *                      LDS-DMA tile (auto's choice for large batches)

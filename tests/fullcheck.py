@@ -49,7 +49,7 @@ def _span(off, size, lo, hi):
 
 def check_all(torch, oracle_mod, alg, keys, d_in, in_off, lens, d_out, out_off, nonces,
               aad, aad_off, aad_len, key_idx=None, chunk=1 << 16, nthreads=None,
-              inner_type=None):
+              inner_type=None, tag=16):
     """Seal records [0, n) of the device batch again with the C oracle and
     compare every output record (ciphertext and tag) with the device's.
 
@@ -61,7 +61,7 @@ def check_all(torch, oracle_mod, alg, keys, d_in, in_off, lens, d_out, out_off, 
     (recordlayer.py:606-617; config 5, equal fragment lengths), so the device
     record at ``out_off[i]`` is lens[i] + 1 + 16 bytes.  Returns the number of
     records and bytes checked; raises Mismatch naming the first records that
-    differ."""
+    differ.  ``tag``: the tag length (8 for AES-CCM_8)."""
     n = len(lens)
     nthreads = nthreads or host_threads()
     in_off = np.asarray(in_off, dtype=np.int64)
@@ -80,7 +80,7 @@ def check_all(torch, oracle_mod, alg, keys, d_in, in_off, lens, d_out, out_off, 
     for lo in range(0, n, chunk):
         hi = min(n, lo + chunk)
         ia, ib = _span(in_off, lens, lo, hi)
-        oa, ob = _span(out_off, lens + extra + 16, lo, hi)
+        oa, ob = _span(out_off, lens + extra + tag, lo, hi)
         h_in = d_in[ia:ib].cpu().numpy()
         h_out = d_out[oa:ob].cpu().numpy()
         r_in_off = in_off[lo:hi] - ia
@@ -100,7 +100,7 @@ def check_all(torch, oracle_mod, alg, keys, d_in, in_off, lens, d_out, out_off, 
                                    aad_len[lo:hi], h_in, r_in_off, r_lens, ob - oa, r_out_off,
                                    key_idx=None if key_idx is None else key_idx[lo:hi],
                                    nthreads=nthreads, out=obuf)
-        rl = r_lens + 16
+        rl = r_lens + tag
         m = hi - lo
         stride = int(r_out_off[1] - r_out_off[0]) if m > 1 else int(rl[0])
         uniform = bool((rl == rl[0]).all()) and stride >= int(rl[0]) and \

@@ -117,6 +117,18 @@ static int check_keys() {
         }
         for (int e = 0; e < 32 * (nr + 1); ++e)
             CHECK(img->bs8mask[e] == bs8_mask_word(img->rk, e), "bs8mask %d", e);
+        // the hybrid kernel's rows: plane (r, i, bit) at word 4 (8 r + bit) + i,
+        // folded for the middle rounds; the rotated round keys
+        for (int e = 0; e < 32 * (nr + 1); ++e) {
+            const int r = e >> 5, i = (e >> 3) & 3, bit = e & 7;
+            const uint32_t want = r >= 1 && r < nr ? bs8_fold_word(img->rk, e) : bs8_mask_word(img->rk, e);
+            CHECK(img->bs8rows[4 * (8 * r + bit) + i] == want, "bs8rows %d", e);
+        }
+        for (int w = 4 * 8 * (nr + 1); w < 15 * 32; ++w) CHECK(img->bs8rows[w] == 0, "bs8rows tail %d", w);
+        for (int w = 0; w < 4 * (nr + 2); ++w) {
+            const uint32_t want = w < 4 * (nr + 1) ? ((img->rk[w] >> 8) | (img->rk[w] << 24)) : img->rk[w - 4];
+            CHECK(img->rkrot[w] == want, "rkrot %d", w);
+        }
         delete img;
     }
     return g_fail;

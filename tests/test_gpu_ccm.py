@@ -157,8 +157,10 @@ def test_batch_fixtures(torch, tg, bi):
 
 
 def test_large_roundtrip_and_samples(torch, tg, oracle_mod):
-    """2^18 x 16 KiB AES-128-CCM records: seal -> open round trip, 32 sampled
-    records bit-exact vs the oracle."""
+    """2^18 x 16 KiB AES-128-CCM records: seal -> open round trip, every
+    record's ciphertext and tag against the threaded C oracle
+    (tests/fullcheck.py), and 32 sampled records through its per-record
+    entry point."""
     n, L, tl = 1 << 18, 16384, 16
     g = torch.Generator(device="cuda").manual_seed(0xcc)
     inp = torch.randint(0, 256, (n * L,), dtype=torch.uint8, device="cuda", generator=g)
@@ -180,11 +182,18 @@ def test_large_roundtrip_and_samples(torch, tg, oracle_mod):
     torch.cuda.synchronize()
     assert int(status.sum()) == n
     assert torch.equal(back, inp)
+    del back
+    import fullcheck   # every record against the oracle (aesccm.py:85-113 restated)
+    recs, _ = fullcheck.check_all(torch, oracle_mod, "aesccm", np.frombuffer(key, np.uint8), inp,
+                                  np.arange(n) * L, np.full(n, L), sealed, np.arange(n) * (L + tl),
+                                  fullcheck.tls13_nonces(iv, 0, n), np.frombuffer(hdr, np.uint8),
+                                  np.zeros(n), np.full(n, 5), tag=tl)
+    assert recs == n
     rng = np.random.default_rng(2)
     for i in np.unique(np.concatenate([[0, n - 1], rng.integers(0, n, 30)])):
         i = int(i)
         pt = inp[i * L:(i + 1) * L].cpu().numpy().tobytes()
         want = oracle_mod.ccm_seal(key, bytes(tls13_nonce(iv, i)), pt, hdr, tl)
         assert sealed[i * (L + tl):(i + 1) * (L + tl)].cpu().numpy().tobytes() == bytes(want), i
-    del inp, back, sealed
+    del inp, sealed
     torch.cuda.empty_cache()

@@ -14,13 +14,15 @@ pytestmark = pytest.mark.gpu
 
 # auto (length split: octet or wave-per-record kernel for the long records,
 # lane kernel for the rest) / lane kernel for all / octet kernel for all
-@pytest.mark.parametrize("variant,lpr", [(0, 0), (0, 32), (0, 64), (1, 0), (14, 0)])
-def test_config4_full_shape_sampled(oracle_mod, variant, lpr):
+# (kt_hybrid -1: the bitsliced key-grouped kernel instead of the default
+# T-table + bitsliced one for the long records)
+@pytest.mark.parametrize("variant,lpr,hyb", [(0, 0, 0), (0, 0, -1), (0, 64, 0), (1, 0, 0), (14, 0, 0)])
+def test_config4_full_shape_sampled(oracle_mod, variant, lpr, hyb):
     import torch
     import tlsgpu
     if not torch.cuda.is_available():
         pytest.fail("GPU tests need a visible MI355X")
-    with tlsgpu.options(gcm_table_variant=variant, kt_lpr=lpr):
+    with tlsgpu.options(gcm_table_variant=variant, kt_lpr=lpr, kt_hybrid=hyb):
         _run_config4(torch, tlsgpu, oracle_mod)
 
 

@@ -26,7 +26,10 @@
 // LDS: the H^8 tables (64 KiB) + S-box + 4 KiB of record planes per 512-thread
 // workgroup, two workgroups per CU.
 #include <cstdlib>
+#include <map>
+#include <mutex>
 #include <type_traits>
+#include <utility>
 
 #include "aes_bs8.h"
 #include "aes_round.h"
@@ -83,14 +86,16 @@ __device__ __forceinline__ uint32_t wave_min_u32(uint32_t v) {
 // a wave-uniform global copy the setup kernel writes (RkLds::rot: scalar
 // loads, so the LDS pipe the T-table waves are bound by carries no key reads).
 
-template <int NR>
-__device__ __forceinline__ void t_half(uint32_t lane4, const RkLds& rk, const CtrCache& cc,
+// LPR: the lanes per record of the job -- a lane's blocks are LPR apart (8:
+// the single-key hybrid's octets; 32: the key-table hybrid's pairs).
+template <int NR, int LPR = 8, class RK = RkLds>
+__device__ __forceinline__ void t_half(uint32_t lane4, const RK& rk, const CtrCache& cc,
                                        uint32_t c0, bool win, const uint4& wc, uint32_t k0w, int h,
                                        uint4 (&ks)[4]) {
     uint32_t s[4][4];
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
-        const uint32_t ctr = c0 + 8u * (4 * h + q);
+        const uint32_t ctr = c0 + (uint32_t)LPR * (4 * h + q);
         if (win) {   // rounds 1-2 from the window constants (aes_ctr_win)
             const uint32_t A = cc.k0 ^ rotl32(T2<3>((ctr << 24) ^ k0w, lane4), 8);
             s[q][0] = wc.x ^ T0<0>(A, lane4);
@@ -193,13 +198,14 @@ struct TableKeyCtx {    // a key of a key table: the wave's 4-bit H^8 tables in 
 // kc.gmul multiplies by H^LPR), batch beta of the lane holds its blocks
 // rho + LPR (8 beta + j), j = 0..7, so each load / store instruction still
 // moves LPR x 16 consecutive bytes per record (whole 128-byte lines).
-template <int NR, bool OPEN, bool TROLE, class KM, class KC, bool PRE = false, int LPR = 8>
+template <int NR, bool OPEN, bool TROLE, class KM, class KC, bool PRE = false, int LPR = 8,
+          class RKT = RkLds>
 __device__ __forceinline__ void octet_job(const KC& kc, const tg_batch& b,
                                           const uint32_t* __restrict__ order, uint64_t t0,
-                                          uint32_t recw, const RkLds& rkT, uint32_t sbox,
+                                          uint32_t recw, const RKT& rkT, uint32_t sbox,
                                           const KM& km) {
     static_assert(LPR == 8 || LPR == 16 || LPR == 32 || LPR == 64, "lanes per record");
-    static_assert(LPR == 8 || !TROLE, "the T-table role runs octets only");
+    static_assert(LPR == 8 || LPR == 32 || !TROLE, "the T-table role runs octets or pairs");
     constexpr uint32_t kM = LPR - 1, kS = LPR == 8 ? 3 : LPR == 16 ? 4 : LPR == 32 ? 5 : 6;
     const uint32_t* rk = kc.rk();
     const uint32_t lane = threadIdx.x & 63u;
@@ -223,7 +229,8 @@ __device__ __forceinline__ void octet_job(const KC& kc, const tg_batch& b,
     const uint32_t nfull = len >> 4, tail = len & 15, nc = (len + 15) >> 4, na = (alen + 15) >> 4;
     const uint32_t rho = (l + nc + 1u) & kM;   // this lane's ciphertext blocks: rho + LPR v
     const uint32_t recb = recw + (lane >> kS) * 128u;
-    const uint32_t rsub = recw + 1024u + (lane >> kS) * 64u;   // rows 0-1 after round 1's SubBytes
+    // rows 0-1 after round 1's SubBytes, behind the (64 / LPR) records' planes
+    const uint32_t rsub = recw + (64u >> kS) * 128u + (lane >> kS) * 64u;
     const uint32_t lane4 = ((lane & 31u) << 2) | kTeBase;
     CtrCache cc = {0, 0, 0, 0};
     if (TROLE) {
@@ -321,10 +328,12 @@ __device__ __forceinline__ void octet_job(const KC& kc, const tg_batch& b,
         const bool one = !OPEN && __all(!valid || nvl <= 8u * beta + 1u);
         if (TROLE) {
             // through the 256-counter window cache when no lane of the wave
-            // crosses a window in this batch (wave-uniform); two halves of four
-            const bool win = __all(((c0 ^ (c0 + 56u)) >> 8) == 0);
+            // crosses a window in this batch (wave-uniform); two halves of four.
+            // Octets: one window for the batch's counters c0 .. c0 + 56; pairs
+            // (LPR 32): a window per half, c0 + 128 h .. c0 + 128 h + 96.
+            const bool win = __all(((c0 ^ (c0 + 7u * LPR)) >> 8) == 0);
             const uint32_t k0w = rkT.get(0).w;
-            const uint4 wc = win ? win_consts<NR>(lane4, rkT, cc, c0) : make_uint4(0, 0, 0, 0);
+            const uint4 wc = LPR == 8 && win ? win_consts<NR>(lane4, rkT, cc, c0) : make_uint4(0, 0, 0, 0);
 #if defined(TG_T_UNROLL)
 #pragma unroll
 #else
@@ -336,12 +345,19 @@ __device__ __forceinline__ void octet_job(const KC& kc, const tg_batch& b,
                 // the half's payload is loaded before its keystream is computed
                 // (1.3 / 0.6 % for seal / open, profiles/r02/v70_tprefetch/)
                 uint4 dp[4];
-                const bool fast = blk0 < (nfast << 6);
+                const bool fast = blk0 < (nfast << (kS + 3));
                 if (fast && valid) {
 #pragma unroll
-                    for (int q = 0; q < 4; ++q) dp[q] = gload16u(in + 16u * (blk0 + 8u * (4 * h + q)));
+                    for (int q = 0; q < 4; ++q) dp[q] = gload16u(in + 16u * (blk0 + LPR * (4 * h + q)));
                 }
-                t_half<NR>(lane4, rkT, cc, c0, win, wc, k0w, h, ks);
+                if constexpr (LPR == 8) {
+                    t_half<NR>(lane4, rkT, cc, c0, win, wc, k0w, h, ks);
+                } else {
+                    const uint32_t ch = c0 + 4u * LPR * h;
+                    const bool winh = __all(((ch ^ (ch + 3u * LPR)) >> 8) == 0);
+                    const uint4 wch = winh ? win_consts<NR>(lane4, rkT, cc, ch) : make_uint4(0, 0, 0, 0);
+                    t_half<NR, LPR>(lane4, rkT, cc, c0, winh, wch, k0w, h, ks);
+                }
                 consume(ks, blk0, 4 * h, std::integral_constant<int, 4>(), fast ? dp : nullptr);
                 __builtin_amdgcn_sched_barrier(0);
             }
@@ -527,22 +543,32 @@ __global__ __launch_bounds__(THREADS) void gcm_hy_kernel(const GcmKeyDev* __rest
 
 // Stream-ordered setup of the hybrid kernel's scratch: the job counter and a
 // device copy of the batch descriptor.
-// The rows hold the bs8_fold_word planes (KeyPlanesVmemFolded) for rounds
-// 1 .. nr - 1 and the round-key planes for rounds 0 and nr.
-__global__ void hy_setup_kernel(tg_batch b, uint32_t* queue, tg_batch* bcopy,
-                                const GcmKeyDev* __restrict__ key, uint32_t* krows, int nr,
-                                uint32_t* rkrot) {
-    for (int e = threadIdx.x; e < 4 * (nr + 2); e += blockDim.x)   // + the plain last key
-        rkrot[e] = e < 4 * (nr + 1) ? rotl32(key->rk[e], 24) : key->rk[e - 4];
+__global__ void hy_setup_kernel(tg_batch b, uint32_t* queue, tg_batch* bcopy) {
     if (threadIdx.x == 0) {
         *queue = 0;
         *bcopy = b;
     }
-    for (int e = threadIdx.x; e < 32 * (nr + 1); e += blockDim.x) {   // KeyPlanesVmem layout
-        const int r = e >> 5, i = (e >> 3) & 3, bit = e & 7;
-        krows[4 * (8 * r + bit) + i] =
-            r >= 1 && r < nr ? bs8_fold_word(key->rk, e) : key->bs8mask[e];
-    }
+}
+
+// The hybrid launch's 256 bytes of scratch (job counter, batch copy), one
+// buffer per (device, stream) for the life of the process: launches on one
+// stream are ordered, so they can share it, and launches on different streams
+// never do.  (Round 3 allocated it per launch with hipMallocAsync, and built
+// the key rows per launch in the setup kernel; both are gone from the
+// per-call path.)  A stream handle reused after hipStreamDestroy inherits the
+// buffer; the destroyed stream's work has completed by then.
+uint8_t* hy_scratch(hipStream_t s) {
+    static std::mutex mu;
+    static std::map<std::pair<int, hipStream_t>, uint8_t*> pool;
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return nullptr;
+    std::lock_guard<std::mutex> g(mu);
+    auto it = pool.find({dev, s});
+    if (it != pool.end()) return it->second;
+    uint8_t* p = nullptr;
+    if (hipMalloc((void**)&p, 256) != hipSuccess) return nullptr;
+    pool[{dev, s}] = p;
+    return p;
 }
 
 template <int NR, bool OPEN>
@@ -572,29 +598,23 @@ int launch_hy(const GcmKeyDev* key, const tg_batch& b, hipStream_t s, const uint
     const uint32_t prio = opt(kOptHyPrio) == 1 ? 1u : 0u;
     const void* fn = small ? (const void*)gcm_hy_kernel<NR, OPEN, 768> : (const void*)gcm_hy_kernel<NR, OPEN, 1024>;
     if (lds_attr(fn, (int)kHyLds)) return TG_EHIP;
-    // job counter + batch copy + key rows: stream-ordered scratch, so
-    // concurrent batches never share them
-    uint8_t* scratch = nullptr;
-    if (hipMallocAsync((void**)&scratch, 256 + 2048 + 256, s) != hipSuccess) return TG_EHIP;
+    // job counter + batch copy: per-stream scratch (hy_scratch); the key rows
+    // and rotated round keys come with the key (GcmKeyDev::bs8rows, rkrot)
+    uint8_t* scratch = hy_scratch(s);
+    if (!scratch) return TG_EHIP;
     uint32_t* queue = reinterpret_cast<uint32_t*>(scratch);
     tg_batch* bcopy = reinterpret_cast<tg_batch*>(scratch + 64);
-    uint32_t* krows = reinterpret_cast<uint32_t*>(scratch + 256);
-    uint32_t* rkrot = reinterpret_cast<uint32_t*>(scratch + 256 + 2048);   // col_r keys
-    hipLaunchKernelGGL(hy_setup_kernel, dim3(1), dim3(64), 0, s, b, queue, bcopy, key, krows, NR, rkrot);
-    bool ok = hipGetLastError() == hipSuccess;
-    if (ok) {
-        if (small)
-            hipLaunchKernelGGL((gcm_hy_kernel<NR, OPEN, 768>), dim3((unsigned)device_cus()), dim3(768), kHyLds, s,
-                               key, (const tg_batch*)bcopy, order, queue, nt, prio, (const uint4*)krows,
-                               (const uint4*)rkrot);
-        else
-            hipLaunchKernelGGL((gcm_hy_kernel<NR, OPEN, 1024>), dim3((unsigned)device_cus()), dim3(1024), kHyLds,
-                               s, key, (const tg_batch*)bcopy, order, queue, nt, prio, (const uint4*)krows,
-                               (const uint4*)rkrot);
-        ok = hipGetLastError() == hipSuccess;
-    }
-    if (hipFreeAsync(scratch, s) != hipSuccess) return TG_EHIP;
-    return ok ? TG_OK : TG_EHIP;
+    hipLaunchKernelGGL(hy_setup_kernel, dim3(1), dim3(64), 0, s, b, queue, bcopy);
+    if (hipGetLastError() != hipSuccess) return TG_EHIP;
+    const uint4* krows = reinterpret_cast<const uint4*>(key->bs8rows);
+    const uint4* rkrot = reinterpret_cast<const uint4*>(key->rkrot);
+    if (small)
+        hipLaunchKernelGGL((gcm_hy_kernel<NR, OPEN, 768>), dim3((unsigned)device_cus()), dim3(768), kHyLds, s,
+                           key, (const tg_batch*)bcopy, order, queue, nt, prio, krows, rkrot);
+    else
+        hipLaunchKernelGGL((gcm_hy_kernel<NR, OPEN, 1024>), dim3((unsigned)device_cus()), dim3(1024), kHyLds,
+                           s, key, (const tg_batch*)bcopy, order, queue, nt, prio, krows, rkrot);
+    return hipGetLastError() == hipSuccess ? TG_OK : TG_EHIP;
 }
 
 // ---- key tables: key-grouped octet jobs on bitsliced waves ----------------
@@ -654,7 +674,105 @@ __global__ __launch_bounds__(kKtThreads, 4) void gcm_kt_kernel(const GcmTableKey
         bs8::KeyPlanesVmemFolded{{reinterpret_cast<const uint4*>(planes + kKtPlaneWords * k)}});
 }
 
-// Per key, the hybrid kernel's key rows (hy_setup_kernel): the
+// ---- key tables, long records: T-table waves beside bitsliced waves -------
+// The single-key hybrid's two ciphers (gcm_hy_kernel) for a key table: one
+// persistent workgroup of 11 waves per CU; waves 0 .. nt - 1 run the T-table
+// cipher (Te0/Te2 copies at kTeBase, the job key's round keys by scalar
+// loads, its rotated copy from the per-key ``rot`` table), the rest the
+// bitsliced one (the key's folded plane rows).  A job is up to two records of
+// one key (tg_key_job_plan, 32 lanes per record), a wave takes kKthChunk
+// consecutive jobs at a time -- the plan orders jobs by key, so consecutive
+// jobs mostly share their key -- and rebuilds its 4-bit GHASH tables of the
+// key's H^32 (8 KiB, build_table4) only when the key changes.  LDS (160 KiB):
+// eight waves' tables below the Te block, three above it, the S-box and a
+// 384-byte record area per wave (two records' first-state planes and their
+// round-1 rows).  11 waves: the Te block and 11 tables fill the LDS (3 waves
+// per SIMD on three SIMDs, 2 on the fourth; <= 168 VGPRs).
+constexpr int kKthWaves = 11;
+constexpr int kKthThreads = kKthWaves * 64;
+constexpr uint32_t kKthSbox = 2 * 65536 + 3 * 8192;
+constexpr uint32_t kKthRec = kKthSbox + 256;
+constexpr uint32_t kKthRecArea = 384;                   // (64 / 32) x 128 + (64 / 32) x 64
+constexpr size_t kKthLds = kKthRec + kKthWaves * kKthRecArea;
+constexpr uint32_t kKthChunk = 4;
+constexpr int kKthTDefault = 7;
+static_assert(kKthLds <= 163840, "key-table hybrid LDS");
+
+__device__ __forceinline__ uint32_t kth_tab(uint32_t w) {
+    return w < 8 ? w * 8192u : 2u * 65536u + (w - 8u) * 8192u;
+}
+
+template <int NR, bool OPEN>
+__global__ __launch_bounds__(kKthThreads) void gcm_kth_kernel(const GcmTableKey* __restrict__ keys,
+                                                             const uint4* __restrict__ hpow,
+                                                             const uint32_t* __restrict__ planes,
+                                                             const uint4* __restrict__ rot, tg_batch b,
+                                                             const uint32_t* __restrict__ order,
+                                                             const uint32_t* __restrict__ jobpos,
+                                                             const uint32_t* __restrict__ njobs_p,
+                                                             const uint32_t* __restrict__ nlong_p,
+                                                             uint32_t* __restrict__ queue, uint32_t nt) {
+    stage_te(reinterpret_cast<uint32_t*>(g_lds_bs8) + kTeBase / 4);
+    stage_sbox(kKthSbox);
+    __syncthreads();
+    const uint32_t wave = (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    const uint32_t tab = kth_tab(wave), recw = kKthRec + wave * kKthRecArea;
+    const uint32_t njobs = *njobs_p, nlong = *nlong_p;
+    uint32_t cur = 0xffffffffu;   // the key whose tables this wave holds
+    for (;;) {
+        uint32_t j0 = 0;
+        if ((threadIdx.x & 63u) == 0) j0 = atomicAdd(queue, kKthChunk);
+        j0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)j0);
+        if (j0 >= njobs) break;
+        const uint32_t j1 = j0 + kKthChunk < njobs ? j0 + kKthChunk : njobs;
+        bool tail = false;
+        for (uint32_t job = j0; job < j1; ++job) {
+            const uint32_t p0 = gld(jobpos, job), p1 = gld(jobpos, job + 1);
+            // the plan's tail (slots >= nlong) is the lane kernel's, and every
+            // later job lies in it too
+            if (p0 >= nlong) {
+                tail = true;
+                break;
+            }
+            const uint32_t k = (uint32_t)__builtin_amdgcn_readfirstlane((int)gld(b.key_idx, gld(order, p0)));
+            if (k != cur) {
+                __builtin_amdgcn_wave_barrier();   // the previous job's lookups are done
+                build_table4(tab, hpow[64u * k + 31u]);
+                cur = k;
+                __builtin_amdgcn_wave_barrier();
+            }
+            tg_batch bj = b;
+            bj.n = p1;   // the job's slots are p0 .. p1 - 1 (at most two)
+            const TableKeyCtx kc{keys[k].rk, hpow + 64u * k, tab};
+            const bs8::KeyPlanesVmemFolded km{{reinterpret_cast<const uint4*>(planes + kKtPlaneWords * k)}};
+            if (wave < nt)
+                octet_job<NR, OPEN, true, bs8::KeyPlanesVmemFolded, TableKeyCtx, false, 32, RkTab>(
+                    kc, bj, order, p0, recw, RkTab{keys[k].rk, rot + 16u * k}, kKthSbox, km);
+            else
+                octet_job<NR, OPEN, false, bs8::KeyPlanesVmemFolded, TableKeyCtx, false, 32>(
+                    kc, bj, order, p0, recw, RkLds{0}, kKthSbox, km);
+        }
+        if (tail) break;
+    }
+}
+
+// Per key, the T-table waves' rotated round keys: rot[16 k + r] = rotr8 of
+// round key r (r = 0 .. nr, aes_round.h col_r), rot[16 k + nr + 1] = the
+// plain last round key (t_half reads it after the rotated ones).
+__global__ void kt_rot_kernel(const GcmTableKey* __restrict__ keys, uint64_t n, int nr, uint32_t* __restrict__ rot) {
+    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const uint64_t k = t / 64;
+    const int e = (int)(t % 64);
+    if (k >= n) return;
+    uint32_t w = 0;
+    if (e < 4 * (nr + 1))
+        w = rotl32(keys[k].rk[e], 24);
+    else if (e < 4 * (nr + 2))
+        w = keys[k].rk[e - 4];
+    rot[64 * k + e] = w;
+}
+
+// Per key, the hybrid kernel's key rows (keymath.h bs8_row_word): the
 // MixColumns-folded planes (keymath.h bs8_fold_word) of rounds 1 .. nr - 1 and
 // the round-key planes of rounds 0 and nr, row (8 r + bit) = the four rows' words.
 __global__ void kt_planes_kernel(const GcmTableKey* __restrict__ keys, uint64_t n, int nr,
@@ -677,6 +795,20 @@ __global__ void kt_planes_kernel(const GcmTableKey* __restrict__ keys, uint64_t 
 // (aes_gcm.hip gcm_table_vkernel) over the tail of the same plan, which the
 // planner leaves sorted by length, longest first.  split 0: every in-range
 // record takes the octet kernel; split ~0u: every record the lane kernel.
+template <int NR, bool OPEN>
+int launch_kth(const GcmTableKey* keys, const uint4* hpow, const uint32_t* planes, const uint4* rot,
+               const tg_batch& b, hipStream_t s, const uint32_t* order, const uint32_t* jobpos,
+               const uint32_t* njobs, const uint32_t* nlong, uint32_t* queue) {
+    const int t = opt(kOptKtT);
+    if (t < 0 || t > kKthWaves) return TG_EINVAL;
+    const uint32_t nt = t ? (uint32_t)t : (uint32_t)kKthTDefault;
+    if (lds_attr((const void*)gcm_kth_kernel<NR, OPEN>, (int)kKthLds)) return TG_EHIP;
+    if (hipMemsetAsync(queue, 0, 4, s) != hipSuccess) return TG_EHIP;
+    hipLaunchKernelGGL((gcm_kth_kernel<NR, OPEN>), dim3((unsigned)device_cus()), dim3(kKthThreads), kKthLds, s,
+                       keys, hpow, planes, rot, b, order, jobpos, njobs, nlong, queue, nt);
+    return hipGetLastError() == hipSuccess ? TG_OK : TG_EHIP;
+}
+
 template <int NR, bool OPEN, int LPR>
 int launch_kt_jobs(const GcmTableKey* keys, uint64_t nkeys, const uint4* hpow, const uint32_t* planes,
                    const tg_batch& b, hipStream_t s, const uint32_t* order, const uint32_t* jobpos,
@@ -705,7 +837,7 @@ int launch_kt_jobs(const GcmTableKey* keys, uint64_t nkeys, const uint4* hpow, c
 // record takes the long kernel; split ~0u: every record the lane kernel.
 template <int NR, bool OPEN>
 int launch_kt(const GcmTableKey* keys, uint64_t nkeys, const uint4* hpow, const uint32_t* planes,
-              const tg_batch& b, hipStream_t s, uint32_t split, int lpr) {
+              const uint4* rot, const tg_batch& b, hipStream_t s, uint32_t split, int lpr, bool hybrid) {
     if (b.n == 0) return TG_OK;
     if (b.n > 0xfffffffeull || !b.key_idx) return TG_EINVAL;
     if (lpr != 0 && lpr != 8 && lpr != 16 && lpr != 32 && lpr != 64) return TG_EINVAL;
@@ -730,7 +862,12 @@ int launch_kt(const GcmTableKey* keys, uint64_t nkeys, const uint4* hpow, const 
                 break;
             case 8: rc = launch_kt_jobs<NR, OPEN, 8>(keys, nkeys, hpow, planes, b, s, order, jobpos, njobs, nlong); break;
             case 16: rc = launch_kt_jobs<NR, OPEN, 16>(keys, nkeys, hpow, planes, b, s, order, jobpos, njobs, nlong); break;
-            case 32: rc = launch_kt_jobs<NR, OPEN, 32>(keys, nkeys, hpow, planes, b, s, order, jobpos, njobs, nlong); break;
+            case 32:
+                rc = hybrid ? launch_kth<NR, OPEN>(keys, hpow, planes, rot, b, s, order, jobpos, njobs, nlong,
+                                                   njobs + 16)
+                            : launch_kt_jobs<NR, OPEN, 32>(keys, nkeys, hpow, planes, b, s, order, jobpos, njobs,
+                                                           nlong);
+                break;
             default: rc = launch_kt_jobs<NR, OPEN, 64>(keys, nkeys, hpow, planes, b, s, order, jobpos, njobs, nlong); break;
         }
     }
@@ -761,20 +898,24 @@ int tg_launch_gcm_bs8(const tg::GcmKeyDev* key, int rounds, const tg_batch& b, b
 }
 
 int tg_launch_gcm_kt(const tg::GcmTableKey* keys, uint64_t nkeys, const uint4* hpow, const uint32_t* planes,
-                     int rounds, const tg_batch& b, bool open, hipStream_t s, uint32_t split, int lpr) {
+                     const uint4* rot, int rounds, const tg_batch& b, bool open, hipStream_t s, uint32_t split,
+                     int lpr, bool hybrid) {
     if (rounds == 10)
-        return open ? tg::launch_kt<10, true>(keys, nkeys, hpow, planes, b, s, split, lpr)
-                    : tg::launch_kt<10, false>(keys, nkeys, hpow, planes, b, s, split, lpr);
+        return open ? tg::launch_kt<10, true>(keys, nkeys, hpow, planes, rot, b, s, split, lpr, hybrid)
+                    : tg::launch_kt<10, false>(keys, nkeys, hpow, planes, rot, b, s, split, lpr, hybrid);
     if (rounds == 14)
-        return open ? tg::launch_kt<14, true>(keys, nkeys, hpow, planes, b, s, split, lpr)
-                    : tg::launch_kt<14, false>(keys, nkeys, hpow, planes, b, s, split, lpr);
+        return open ? tg::launch_kt<14, true>(keys, nkeys, hpow, planes, rot, b, s, split, lpr, hybrid)
+                    : tg::launch_kt<14, false>(keys, nkeys, hpow, planes, rot, b, s, split, lpr, hybrid);
     return TG_EINVAL;
 }
 
 int tg_launch_kt_planes(const tg::GcmTableKey* keys, uint64_t n, int rounds, uint32_t* planes,
-                        hipStream_t s) {
+                        uint4* rot, hipStream_t s) {
     const uint64_t total = n * tg::kKtPlaneWords;
     hipLaunchKernelGGL(tg::kt_planes_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, keys, n,
                        rounds, planes);
+    if (hipGetLastError() != hipSuccess) return TG_EHIP;
+    hipLaunchKernelGGL(tg::kt_rot_kernel, dim3((unsigned)((n * 64 + 255) / 256)), dim3(256), 0, s, keys, n,
+                       rounds, reinterpret_cast<uint32_t*>(rot));
     return hipGetLastError() == hipSuccess ? TG_OK : TG_EHIP;
 }

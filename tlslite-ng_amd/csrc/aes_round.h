@@ -139,6 +139,16 @@ struct RkLds {  // key table: this lane's schedule staged in an LDS row
     // volatile: re-read per round instead of being hoisted into 60 VGPRs
     __device__ __forceinline__ uint4 get(int r) const { return lds_u128_v(base + 16 * r); }
 };
+// A wave-uniform key of a key table in global memory (scalar loads): the
+// schedule words ``rk`` (GcmTableKey::rk) and the rotated copy ``rot`` (the
+// key-table hybrid kernel's T-table waves, aes_gcm_bs8.hip).
+struct RkTab {
+    const uint32_t* rk;
+    const uint4* rot;
+    __device__ __forceinline__ uint4 get(int r) const {
+        return make_uint4(rk[4 * r], rk[4 * r + 1], rk[4 * r + 2], rk[4 * r + 3]);
+    }
+};
 
 // Per-record round-1 constants for counter mode: after AddRoundKey the state
 // words s0..s2 (nonce ^ rk0) are the same for every block of the record, so

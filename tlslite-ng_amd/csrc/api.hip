@@ -57,6 +57,8 @@ TG_SAME_OFFSET(hpow);
 TG_SAME_OFFSET(ghash64);
 TG_SAME_OFFSET(ghash8);
 TG_SAME_OFFSET(bs8mask);
+TG_SAME_OFFSET(bs8rows);
+TG_SAME_OFFSET(rkrot);
 #undef TG_SAME_OFFSET
 
 }  // namespace
@@ -171,9 +173,11 @@ bool is_ccm(int alg) { return alg == TG_AES_CCM || alg == TG_AES_CCM_8; }
 // A multi-key AES-GCM allocation: GcmTableKey[nkeys], then the 64 GHASH
 // powers of each key (gcm_table_wave_kernel, gcm_kt_kernel), then the 15 x 32
 // bitsliced key-plane words of each key, MixColumns-folded, in the hybrid
-// kernel's row layout (gcm_kt_kernel, kt_planes_kernel).
+// kernel's row layout (gcm_kt_kernel, kt_planes_kernel), then 16 rotated
+// round-key words x 4 per key (gcm_kth_kernel's T-table waves, kt_rot_kernel).
 constexpr size_t kTableHpowBytes = 64 * sizeof(uint4);
 constexpr size_t kTablePlaneBytes = 15 * 32 * sizeof(uint32_t);
+constexpr size_t kTableRotBytes = 16 * sizeof(uint4);
 uint4* table_hpow(const tg_key* k) {
     return reinterpret_cast<uint4*>(static_cast<uint8_t*>(k->dev_key) +
                                     sizeof(tg::GcmTableKey) * k->nkeys);
@@ -182,19 +186,22 @@ uint32_t* table_planes(const tg_key* k) {
     return reinterpret_cast<uint32_t*>(reinterpret_cast<uint8_t*>(table_hpow(k)) +
                                        kTableHpowBytes * k->nkeys);
 }
+uint4* table_rot(const tg_key* k) {
+    return reinterpret_cast<uint4*>(reinterpret_cast<uint8_t*>(table_planes(k)) + kTablePlaneBytes * k->nkeys);
+}
 
 // The table's derived arrays on the device: H^1..H^64 and the key planes.
 int table_derive(tg_key* k, hipStream_t s) {
     const auto* keys = static_cast<const tg::GcmTableKey*>(k->dev_key);
     int rc = tg_launch_table_hpow(keys, k->nkeys, table_hpow(k), s);
-    if (!rc) rc = tg_launch_kt_planes(keys, k->nkeys, k->rounds, table_planes(k), s);
+    if (!rc) rc = tg_launch_kt_planes(keys, k->nkeys, k->rounds, table_planes(k), table_rot(k), s);
     return rc;
 }
 
 size_t dev_key_bytes(const tg_key* k) {
     if (k->alg == TG_CHACHA20_POLY1305) return sizeof(tg::ChachaKeyDev) * k->nkeys;
     if (is_ccm(k->alg)) return sizeof(tg::AesKeyDev) * k->nkeys;
-    return k->nkeys > 1 ? (sizeof(tg::GcmTableKey) + kTableHpowBytes + kTablePlaneBytes) * k->nkeys
+    return k->nkeys > 1 ? (sizeof(tg::GcmTableKey) + kTableHpowBytes + kTablePlaneBytes + kTableRotBytes) * k->nkeys
                         : sizeof(tg::GcmKeyDev);
 }
 
@@ -241,7 +248,11 @@ int launch_gcm_table(tg_key* k, const tg_batch& b, bool open, hipStream_t s) {
         case 14: split = 0; lpr = 8; break;
         default: return TG_EINVAL;
     }
-    return tg_launch_gcm_kt(keys, k->nkeys, table_hpow(k), table_planes(k), k->rounds, b, open, s, split, lpr);
+    // the long records (lpr 32) on the T-table + bitsliced kernel unless
+    // kt_hybrid = -1 (the bitsliced-only key-grouped kernel)
+    const bool hybrid = lpr == 32 && tg::opt(tg::kOptKtHybrid) >= 0;
+    return tg_launch_gcm_kt(keys, k->nkeys, table_hpow(k), table_planes(k), table_rot(k), k->rounds, b, open, s,
+                            split, lpr, hybrid);
 }
 
 // The order and the sort's scratch are allocated stream-ordered on the

@@ -61,6 +61,11 @@ struct GcmKeyDev {
     uint4 ghash8[kGhashEntries];    // the 8-bit tables of H^8 (gcm_bs8_kernel's stride)
     // 8-block bitsliced AES (aes_bs8.h): round-key plane (r, i, b) at (4 r + i) 8 + b
     uint32_t bs8mask[15 * 32];
+    // the hybrid kernel's key material, built with the key: the bitsliced
+    // waves' key rows (keymath.h bs8_row_word) and the T-table waves' rotated
+    // round keys (rkrot_word)
+    uint32_t bs8rows[15 * 32];
+    uint32_t rkrot[64];
 };
 
 // Powers of H for the wave-per-record kernel: hpow[e - 1] = H^e in normal
@@ -321,9 +326,12 @@ int tg_key_job_plan(const uint32_t* key_idx, const uint32_t* len, uint32_t fixed
 // H^1..H^64), the others through the lane kernel.
 // lpr: lanes per record of the key-grouped bitsliced kernel for the long
 // records (8, 16, 32 or 64), or 0 for the wave-per-record T-table kernel
-// with per-wave 4-bit GHASH tables.
+// with per-wave 4-bit GHASH tables.  hybrid (lpr 32 only): the long records on
+// the persistent T-table + bitsliced kernel (rot = the keys' rotated round
+// keys, tg_launch_kt_planes).
 int tg_launch_gcm_kt(const tg::GcmTableKey* keys, uint64_t nkeys, const uint4* hpow, const uint32_t* planes,
-                     int rounds, const tg_batch& b, bool open, hipStream_t s, uint32_t split, int lpr);
+                     const uint4* rot, int rounds, const tg_batch& b, bool open, hipStream_t s, uint32_t split,
+                     int lpr, bool hybrid);
 // The key-table lane kernel over slots [*first, n) of ``order`` (first NULL:
 // all of them) and the key-table wave-per-record kernel (aes_gcm.hip).
 int tg_launch_gcm_table_lane(const tg::GcmTableKey* keys, uint64_t nkeys, int rounds, const tg_batch& b,
@@ -333,8 +341,10 @@ int tg_launch_gcm_table_lane(const tg::GcmTableKey* keys, uint64_t nkeys, int ro
 int tg_launch_gcm_table_wave(const tg::GcmTableKey* keys, uint64_t nkeys, const uint4* hpow, int rounds,
                              const tg_batch& b, bool open, hipStream_t s, bool t4,
                              const uint32_t* order = nullptr, const uint32_t* count = nullptr);
+// The key table's bitsliced key rows (planes) and the T-table waves' rotated
+// round keys (rot, 16 x 16 bytes per key).
 int tg_launch_kt_planes(const tg::GcmTableKey* keys, uint64_t n, int rounds, uint32_t* planes,
-                        hipStream_t s);
+                        uint4* rot, hipStream_t s);
 int tg_launch_ccm(const tg::AesKeyDev* keys, uint64_t nkeys, int rounds, int taglen,
                   const tg_batch& b, bool open, hipStream_t s);
 // Whether a single-key batch of n records runs the wave-per-record kernel

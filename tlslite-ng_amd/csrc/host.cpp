@@ -184,6 +184,8 @@ int gcm_key_image(const uint8_t* key, size_t keylen, GcmKeyImage* out) {
     from_norm(out->hpow[7], hb);                        // tables of H^8 (octet kernels)
     ghash_tables(hb, out->ghash8);
     for (int e = 0; e < 32 * (nr + 1); ++e) out->bs8mask[e] = bs8_mask_word(out->rk, e);
+    for (int w = 0; w < 15 * 32; ++w) out->bs8rows[w] = bs8_row_word(out->rk, nr, w);
+    for (int w = 0; w < 64; ++w) out->rkrot[w] = rkrot_word(out->rk, nr, w);
     memset(rkb, 0, sizeof(rkb));
     memset(h, 0, sizeof(h));
     memset(hb, 0, sizeof(hb));

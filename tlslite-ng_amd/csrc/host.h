@@ -20,6 +20,11 @@ struct GcmKeyImage {
     uint32_t ghash64[16 * 256][4];
     uint32_t ghash8[16 * 256][4];
     uint32_t bs8mask[15 * 32];
+    // the hybrid kernel's key material, built with the key: the bitsliced
+    // waves' key rows (keymath.h bs8_row_word) and the T-table waves' rotated
+    // round keys (rkrot_word)
+    uint32_t bs8rows[15 * 32];
+    uint32_t rkrot[64];
 };
 
 uint32_t le32(const uint8_t* p);

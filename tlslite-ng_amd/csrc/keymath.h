@@ -108,4 +108,24 @@ TG_KM_HD uint32_t bs8_fold_word(const uint32_t* rk, int e) {
     return m;
 }
 
+// Word w = 4 (8 r + bit) + i of the hybrid kernel's bitsliced key rows
+// (aes_bs8.h KeyPlanesVmem row layout, GcmKeyDev::bs8rows): the
+// MixColumns-folded planes (bs8_fold_word) of rounds 1 .. nr - 1, the plain
+// planes (bs8_mask_word) of rounds 0 and nr, zero past them.
+TG_KM_HD uint32_t bs8_row_word(const uint32_t* rk, int nr, int w) {
+    const int row = w >> 2, i = w & 3, r = row >> 3, bit = row & 7;
+    if (r > nr) return 0;
+    const int e = 32 * r + 8 * i + bit;
+    return r >= 1 && r < nr ? bs8_fold_word(rk, e) : bs8_mask_word(rk, e);
+}
+
+// Word w of the T-table waves' round keys (GcmKeyDev::rkrot): round key r
+// rotated right by 8 bits for r = 0 .. nr (aes_round.h col_r), then the plain
+// last round key; zero past it.
+TG_KM_HD uint32_t rkrot_word(const uint32_t* rk, int nr, int w) {
+    if (w < 4 * (nr + 1)) return (rk[w] >> 8) | (rk[w] << 24);
+    if (w < 4 * (nr + 2)) return rk[w - 4];
+    return 0;
+}
+
 }  // namespace tg

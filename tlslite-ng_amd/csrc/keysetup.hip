@@ -373,7 +373,10 @@ __global__ void hpow_kernel(GcmKeyDev* key) {
 // 32 (NR + 1) <= 480 planes.
 __global__ void bs_mask_kernel(GcmKeyDev* key) {
     const int e = blockIdx.x * blockDim.x + threadIdx.x;
-    if (e < 32 * (int)(key->rounds + 1)) key->bs8mask[e] = bs8::mask_word(key->rk, e);
+    const int nr = (int)key->rounds;
+    if (e < 32 * (nr + 1)) key->bs8mask[e] = bs8::mask_word(key->rk, e);
+    if (e < 15 * 32) key->bs8rows[e] = bs8_row_word(key->rk, nr, e);   // the hybrid's key rows
+    if (e < 64) key->rkrot[e] = rkrot_word(key->rk, nr, e);
 }
 
 }  // namespace

@@ -27,6 +27,8 @@ constexpr OptName kNames[kOptCount] = {
     {"kt_split", "TLSGPU_KT_SPLIT"},
     {"kt_lpr", "TLSGPU_KT_LPR"},
     {"hy_threads", "TLSGPU_HY_THREADS"},
+    {"kt_hybrid", "TLSGPU_KT_HYBRID"},
+    {"kt_t", "TLSGPU_KT_T"},
 };
 
 std::atomic<int> g_val[kOptCount];

@@ -23,6 +23,9 @@ enum Opt {
     kOptKtLpr,                // TLSGPU_KT_LPR: key-table long records, lanes per record
                               // (8 / 16 / 32 / 64), -1 wave-per-record T-table, 0 auto
     kOptHyThreads,            // TLSGPU_HY_THREADS: hybrid AES-GCM workgroup, 0 = 1024, or 768
+    kOptKtHybrid,             // TLSGPU_KT_HYBRID: key-table long records on the T-table +
+                              // bitsliced persistent kernel (1) or the bitsliced one (-1), 0 auto
+    kOptKtT,                  // TLSGPU_KT_T: T-table waves of that kernel (0 = auto)
     kOptCount
 };
 
