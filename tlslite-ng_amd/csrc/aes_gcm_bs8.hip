@@ -270,9 +270,18 @@ __device__ __forceinline__ void octet_job(const KC& kc, const tg_batch& b,
     }
 
     // the bitsliced cipher leaves out the last round key (folded into the XOR)
-    const uint4 rkl = TROLE ? make_uint4(0, 0, 0, 0)
-                            : make_uint4(rk[4 * NR] ^ 0x63636363u, rk[4 * NR + 1] ^ 0x63636363u,
-                                         rk[4 * NR + 2] ^ 0x63636363u, rk[4 * NR + 3] ^ 0x63636363u);
+    // (KeyPlanesVec: by a vector load, so consume()'s 3-input XORs take it
+    // from VGPRs at full rate instead of from SGPRs at half rate)
+    uint4 rkl = make_uint4(0, 0, 0, 0);
+    if constexpr (!TROLE) {
+        if constexpr (bs8::round_rows<KM>()) {
+            const uint4 v = gload16(reinterpret_cast<const uint8_t*>(rk + 4 * NR) + km.zv);
+            rkl = make_uint4(v.x ^ 0x63636363u, v.y ^ 0x63636363u, v.z ^ 0x63636363u, v.w ^ 0x63636363u);
+        } else {
+            rkl = make_uint4(rk[4 * NR] ^ 0x63636363u, rk[4 * NR + 1] ^ 0x63636363u,
+                             rk[4 * NR + 2] ^ 0x63636363u, rk[4 * NR + 3] ^ 0x63636363u);
+        }
+    }
     // XOR + store of N consecutive slots j0 .. j0 + N - 1 (the keystream dies
     // block by block), then the GHASH chain over their inputs
     // pre: the slots' payload already loaded (fast path only), else nullptr
@@ -524,9 +533,11 @@ __global__ __launch_bounds__(THREADS) void gcm_hy_kernel(const GcmKeyDev* __rest
                                       kHySbox, bs8::KeyPlanesVmemFolded{{krows}});
         }
     } else {
+        // The key rows by scalar loads (SGPR operands: the T gates issue at
+        // half rate).  Vector loads into VGPRs (bs8::KeyPlanesVec) measured
+        // seal equal and open 3 % slower (spills in the open kernel's loop,
+        // profiles/r04/r4a/aes_ab.txt), so they are not used here.
         const RkLds none{0};
-        uint32_t zv = 0;   // the key rows' vector loads (bs8::KeyPlanesVec)
-        asm volatile("v_mov_b32 %0, 0" : "=v"(zv));
         for (;;) {
             uint32_t job = 0;
             if ((threadIdx.x & 63u) == 0) job = atomicAdd(queue, 1u);
@@ -534,9 +545,9 @@ __global__ __launch_bounds__(THREADS) void gcm_hy_kernel(const GcmKeyDev* __rest
             if (job >= njobs) break;
             asm volatile("" ::: "memory");
             const tg_batch b = *bp;
-            octet_job<NR, OPEN, false, bs8::KeyPlanesVec, SingleKeyRowCtx, (THREADS < 1024)>(
+            octet_job<NR, OPEN, false, bs8::KeyPlanesVmemFolded, SingleKeyRowCtx, (THREADS < 1024)>(
                 SingleKeyRowCtx{key, jw}, b, order, 8ull * job, recw, none, kHySbox,
-                bs8::KeyPlanesVec{krows, zv});
+                bs8::KeyPlanesVmemFolded{{krows}});
         }
     }
 }
