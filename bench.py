@@ -32,6 +32,27 @@ NONCE_LEN = 12
 TAG_LEN = 16
 
 
+# The JSON line goes to the process's original stdout, and only it: once the
+# arguments are parsed, fd 1 is pointed at stderr, so library banners (RCCL
+# prints its version block to fd 1 when a communicator is created) cannot
+# land in the driver's one-line output.
+_JSON_FD = None
+
+
+def emit(line):
+    """Print the bench's one JSON line on the original stdout."""
+    os.write(_JSON_FD if _JSON_FD is not None else 1, (json.dumps(line) + "\n").encode())
+
+
+def quiet_stdout():
+    """Keep fd 1 for the JSON line (emit) and send everything else to stderr."""
+    global _JSON_FD
+    if _JSON_FD is None:
+        sys.stdout.flush()
+        _JSON_FD = os.dup(1)
+        os.dup2(2, 1)
+
+
 def algorithmic_bytes(n, L, op):
     """seal reads L + A + 12, writes L + 16; open reads
     L + 16 + A + 12, writes L (+1 status byte)."""
@@ -230,7 +251,7 @@ def main():
                     help="CPU baseline: seconds each process seals/opens")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--e2e", action="store_true", help="also time the host<->device path")
-    ap.add_argument("--traffic-file", default=os.path.join(ROOT, "profiles", "r03", "traffic.json"),
+    ap.add_argument("--traffic-file", default=os.path.join(ROOT, "profiles", "r04", "traffic.json"),
                     help="per-launch HBM bytes from tools/traffic.sh (rocprofv3 FETCH_SIZE / "
                          "WRITE_SIZE passes at this config, calibrated per access shape) for "
                          "roofline.traffic")
@@ -278,6 +299,7 @@ def main():
     if err:
         print(err, file=sys.stderr)
         sys.exit(2)
+    quiet_stdout()
     if args.dist_selftest:
         os.environ["TLSGPU_DIST_SELFTEST"] = "1"
     if args.config == "ingest":
@@ -443,7 +465,7 @@ def main():
             cores = args.cpu_cores or host_cores()[0]
             line["cpu_baseline"] = cpu_baseline(L, cores, args.cpu_seconds, samples)
             line["cpu_baseline"]["config1"] = cpu_config1(cores)
-        print(json.dumps(line), flush=True)
+        emit(line)
     if tgd.group_active(dist):
         dist.destroy_process_group()
     if not ok:
@@ -481,7 +503,7 @@ def c4_traffic(path, op):
     if not all(parts):
         return None
     return {"hbm_bytes": round(sum(k["hbm_bytes"] for k in parts)),
-            "kernels": {"gcm_kt_kernel": round(parts[0]["hbm_bytes"]),
+            "kernels": {"long_records (gcm_kth_kernel)": round(parts[0]["hbm_bytes"]),
                         "gcm_table_vkernel": round(parts[1]["hbm_bytes"])},
             "source": os.path.relpath(path, ROOT)}
 
@@ -663,7 +685,7 @@ def run_config1(args):
             "sealed_sha256": digest, "digest_match": digest == want, "verified": bool(ok)}
     if not args.no_cpu_baseline:
         line["cpu_baseline"] = cpu_config1(args.cpu_cores or host_cores()[0])
-    print(json.dumps(line), flush=True)
+    emit(line)
     if not ok:
         sys.exit(3)
 
@@ -770,7 +792,7 @@ def run_config5(args):
         if not args.no_cpu_baseline and world == 1:
             cores = args.cpu_cores or host_cores()[0]
             line["cpu_baseline"] = cpu_baseline_c5(L, cores, args.cpu_seconds)
-        print(json.dumps(line), flush=True)
+        emit(line)
     if tgd.group_active(dist):
         dist.destroy_process_group()
     if not ok:
@@ -871,7 +893,7 @@ def run_config4(args):
         tr["traffic_over_algorithmic"] = round(tr["hbm_bytes"] / alg, 3)
         line["roofline"]["traffic"] = tr["hbm_bytes"]
         line["roofline"]["traffic_detail"] = tr
-    print(json.dumps(line), flush=True)
+    emit(line)
     if not ok:
         sys.exit(3)
 
@@ -954,7 +976,7 @@ def run_ingest(args):
                       "16 KiB records, host memory to host memory",
             "unit": "GiB/s", "n_gpus": 1, "app_data_bytes": total, "dtype": "u8",
             "data": "synthetic", "per_alg": res}
-    print(json.dumps(line), flush=True)
+    emit(line)
 
 
 def pcie_ceiling(torch, nbytes=1 << 30):

@@ -15,7 +15,8 @@ factors of its shape:
   chacha20-poly1305_* chacha_kernel, line-pair tile: the same 8 records x
                       128 B per instruction -> the octet factors (round 1's
                       tile moved 16 records x 64 B: tile64)
-  c4_kt_*             gcm_kt_kernel (config 4's long records), octet layout
+  c4_kt_*             gcm_kth_kernel (round 4; gcm_kt_kernel before: config 4's
+                      long records), whole-line layout -> the octet factors
   c4_lane_*           gcm_table_vkernel (config 4's short records), 16 B per
                       lane, one record per lane -> the lane factors
   c5_prep, c5_seal    config 5 (bench.py --config c5, collected from its own
@@ -48,6 +49,10 @@ KERNELS = [(r"gcm_hy_kernel<10, false", "aes128gcm_seal", "octet", "octet"),
            (r"chacha_kernel<true", "chacha20-poly1305_open", "line-pair tile", "octet"),
            (r"gcm_kt_kernel<14, false", "c4_kt_seal", "octet", "octet"),
            (r"gcm_kt_kernel<14, true", "c4_kt_open", "octet", "octet"),
+           # round 4: the key-table hybrid (long records, 32 lanes per record:
+           # each instruction moves 2 records x 512 B, whole lines -> octet)
+           (r"gcm_kth_kernel<14, false", "c4_kt_seal", "octet", "octet"),
+           (r"gcm_kth_kernel<14, true", "c4_kt_open", "octet", "octet"),
            (r"gcm_table_vkernel<14, false", "c4_lane_seal", "lane", "lane"),
            (r"gcm_table_vkernel<14, true", "c4_lane_open", "lane", "lane")]
 KERNELS_C5 = [(r"seal_prep", "c5_prep", "lane", "lane"),
