@@ -70,31 +70,41 @@ int tg_launch_zero_skipped(const tg_batch& b, uint64_t nkeys, hipStream_t s) {
 namespace {
 
 // Sort key: (key, length descending); records shorter than ``split`` or with
-// a key index not below nkeys get the tail key kTail (sorted last, by length).
-constexpr uint32_t kTail = 0xffffffffu;
-
+// a key index not below nkeys get the tail key nkeys (sorted last, by length).
+// Packed as g << LB | (max - L) in a K: with a 32-bit K the length keeps LB =
+// 32 - bits(nkeys) bits (longer records sort as equal, which only loosens the
+// longest-first order among them), so the radix sort makes 4 passes over
+// 32-bit keys instead of 8 over 64-bit ones (config 4: nkeys = 65 536, LB =
+// 15, every TLS record length fits).
+template <class K>
 __global__ void kjp_keys(const uint32_t* __restrict__ key_idx, const uint32_t* __restrict__ len,
-                         uint32_t fixed_len, uint64_t n, uint64_t nkeys, uint32_t split,
-                         uint64_t* __restrict__ ck, uint32_t* __restrict__ nlong) {
+                         uint32_t fixed_len, uint64_t n, uint64_t nkeys, uint32_t split, int lb,
+                         K* __restrict__ ck, uint32_t* __restrict__ nlong) {
     const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (t == 0) *nlong = (uint32_t)n;   // no tail unless kjp_tail finds one
     if (t >= n) return;
     const uint32_t L = len ? len[t] : fixed_len;
     const uint32_t k = key_idx[t];
-    const uint32_t g = (k >= nkeys || L < split) ? kTail : k;
-    ck[t] = ((uint64_t)g << 32) | (uint64_t)(0xffffffffu - L);
+    const uint64_t g = (k >= nkeys || L < split) ? nkeys : k;
+    const uint64_t lmax = lb >= 32 ? 0xffffffffull : (1ull << lb) - 1u;
+    const uint64_t Lc = L < lmax ? L : lmax;
+    ck[t] = (K)((g << lb) | (lmax - Lc));
 }
 
-__global__ void kjp_tail(const uint64_t* __restrict__ ck, uint64_t n, uint32_t* __restrict__ nlong) {
+template <class K>
+__global__ void kjp_tail(const K* __restrict__ ck, uint64_t n, uint64_t nkeys, int lb,
+                         uint32_t* __restrict__ nlong) {
     const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= n) return;
-    if ((ck[t] >> 32) == kTail && (t == 0 || (ck[t - 1] >> 32) != kTail)) *nlong = (uint32_t)t;
+    if ((uint64_t)(ck[t] >> lb) == nkeys && (t == 0 || (uint64_t)(ck[t - 1] >> lb) != nkeys))
+        *nlong = (uint32_t)t;
 }
 
-__global__ void kjp_group_starts(const uint64_t* __restrict__ ck, uint64_t n, uint32_t* __restrict__ g) {
+template <class K>
+__global__ void kjp_group_starts(const K* __restrict__ ck, uint64_t n, int lb, uint32_t* __restrict__ g) {
     const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= n) return;
-    g[t] = (t == 0 || (ck[t] >> 32) != (ck[t - 1] >> 32)) ? (uint32_t)t : 0u;
+    g[t] = (t == 0 || (ck[t] >> lb) != (ck[t - 1] >> lb)) ? (uint32_t)t : 0u;
 }
 
 __global__ void kjp_job_starts(const uint32_t* __restrict__ gs, uint64_t n, uint32_t jobsz,
@@ -115,6 +125,21 @@ __global__ void kjp_scatter(const uint32_t* __restrict__ js, const uint32_t* __r
     }
 }
 
+int bit_width(uint64_t v) {
+    int b = 0;
+    while (v) {
+        ++b;
+        v >>= 1;
+    }
+    return b;
+}
+
+// The plan with K-wide sort keys (see kjp_keys).
+template <class K>
+int key_job_plan(const uint32_t* key_idx, const uint32_t* len, uint32_t fixed_len, uint64_t n,
+                 uint64_t nkeys, uint32_t split, uint32_t jobsz, uint32_t* order, uint32_t* jobpos,
+                 uint32_t* njobs, uint32_t* nlong, void* scratch, size_t* bytes, hipStream_t s, int lb);
+
 size_t ru256(size_t v) { return (v + 255) & ~(size_t)255; }
 
 }  // namespace
@@ -129,39 +154,55 @@ int tg_key_job_plan(const uint32_t* key_idx, const uint32_t* len, uint32_t fixed
                     uint64_t nkeys, uint32_t split, uint32_t jobsz, uint32_t* order, uint32_t* jobpos,
                     uint32_t* njobs, uint32_t* nlong, void* scratch, size_t* bytes, hipStream_t s) {
     if (jobsz == 0 || (jobsz & (jobsz - 1u))) return TG_EINVAL;
+    // 32-bit keys when the key index (tail marker nkeys included) leaves at
+    // least 15 bits for the length: 2^14 + 256, the longest TLS record, fits
+    const int kb = bit_width(nkeys);
+    if (kb <= 17)
+        return key_job_plan<uint32_t>(key_idx, len, fixed_len, n, nkeys, split, jobsz, order, jobpos, njobs,
+                                      nlong, scratch, bytes, s, 32 - kb);
+    return key_job_plan<uint64_t>(key_idx, len, fixed_len, n, nkeys, split, jobsz, order, jobpos, njobs, nlong,
+                                  scratch, bytes, s, 32);
+}
+
+namespace {
+template <class K>
+int key_job_plan(const uint32_t* key_idx, const uint32_t* len, uint32_t fixed_len, uint64_t n,
+                 uint64_t nkeys, uint32_t split, uint32_t jobsz, uint32_t* order, uint32_t* jobpos,
+                 uint32_t* njobs, uint32_t* nlong, void* scratch, size_t* bytes, hipStream_t s, int lb) {
     rocprim::counting_iterator<uint32_t> iota(0);
+    const int kbits = lb + bit_width(nkeys);   // significant bits of the sort key
     size_t t_sort = 0, t_max = 0, t_sum = 0;
-    if (rocprim::radix_sort_pairs(nullptr, t_sort, (uint64_t*)nullptr, (uint64_t*)nullptr, iota,
-                                  (uint32_t*)nullptr, (size_t)n, 0, 64, s) != hipSuccess ||
+    if (rocprim::radix_sort_pairs(nullptr, t_sort, (K*)nullptr, (K*)nullptr, iota, (uint32_t*)nullptr, (size_t)n,
+                                  0, kbits, s) != hipSuccess ||
         rocprim::inclusive_scan(nullptr, t_max, (uint32_t*)nullptr, (uint32_t*)nullptr, (size_t)n,
                                 rocprim::maximum<uint32_t>(), s) != hipSuccess ||
         rocprim::inclusive_scan(nullptr, t_sum, (uint32_t*)nullptr, (uint32_t*)nullptr, (size_t)n,
                                 rocprim::plus<uint32_t>(), s) != hipSuccess)
         return TG_EHIP;
-    const size_t b64 = ru256(n * 8), b32 = ru256(n * 4);
+    const size_t bk = ru256(n * sizeof(K)), b32 = ru256(n * 4);
     size_t tmp = t_sort > t_max ? t_sort : t_max;
     tmp = tmp > t_sum ? tmp : t_sum;
-    const size_t need = 2 * b64 + 3 * b32 + ru256(tmp);
+    const size_t need = 2 * bk + 3 * b32 + ru256(tmp);
     if (!scratch) {
         *bytes = need;
         return TG_OK;
     }
     if (*bytes < need || n == 0) return TG_EINVAL;
     uint8_t* p = static_cast<uint8_t*>(scratch);
-    uint64_t* ck = reinterpret_cast<uint64_t*>(p);
-    uint64_t* ck_sorted = reinterpret_cast<uint64_t*>(p + b64);
-    uint32_t* g = reinterpret_cast<uint32_t*>(p + 2 * b64);
-    uint32_t* gs = reinterpret_cast<uint32_t*>(p + 2 * b64 + b32);
-    uint32_t* js = reinterpret_cast<uint32_t*>(p + 2 * b64 + 2 * b32);
-    void* t = p + 2 * b64 + 3 * b32;
+    K* ck = reinterpret_cast<K*>(p);
+    K* ck_sorted = reinterpret_cast<K*>(p + bk);
+    uint32_t* g = reinterpret_cast<uint32_t*>(p + 2 * bk);
+    uint32_t* gs = reinterpret_cast<uint32_t*>(p + 2 * bk + b32);
+    uint32_t* js = reinterpret_cast<uint32_t*>(p + 2 * bk + 2 * b32);
+    void* t = p + 2 * bk + 3 * b32;
     const unsigned blocks = (unsigned)((n + 255) / 256);
-    hipLaunchKernelGGL(kjp_keys, dim3(blocks), dim3(256), 0, s, key_idx, len, fixed_len, n, nkeys, split,
+    hipLaunchKernelGGL((kjp_keys<K>), dim3(blocks), dim3(256), 0, s, key_idx, len, fixed_len, n, nkeys, split, lb,
                        ck, nlong);
     size_t ts = t_sort;
-    if (rocprim::radix_sort_pairs(t, ts, ck, ck_sorted, iota, order, (size_t)n, 0, 64, s) != hipSuccess)
+    if (rocprim::radix_sort_pairs(t, ts, ck, ck_sorted, iota, order, (size_t)n, 0, kbits, s) != hipSuccess)
         return TG_EHIP;
-    hipLaunchKernelGGL(kjp_tail, dim3(blocks), dim3(256), 0, s, ck_sorted, n, nlong);
-    hipLaunchKernelGGL(kjp_group_starts, dim3(blocks), dim3(256), 0, s, ck_sorted, n, g);
+    hipLaunchKernelGGL((kjp_tail<K>), dim3(blocks), dim3(256), 0, s, ck_sorted, n, nkeys, lb, nlong);
+    hipLaunchKernelGGL((kjp_group_starts<K>), dim3(blocks), dim3(256), 0, s, ck_sorted, n, lb, g);
     size_t tm = t_max;
     if (rocprim::inclusive_scan(t, tm, g, gs, (size_t)n, rocprim::maximum<uint32_t>(), s) != hipSuccess)
         return TG_EHIP;
@@ -173,3 +214,4 @@ int tg_key_job_plan(const uint32_t* key_idx, const uint32_t* len, uint32_t fixed
     hipLaunchKernelGGL(kjp_scatter, dim3(blocks), dim3(256), 0, s, js, jx, n, jobpos, njobs);
     return hipGetLastError() == hipSuccess ? TG_OK : TG_EHIP;
 }
+}  // namespace
