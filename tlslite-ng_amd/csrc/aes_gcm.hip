@@ -430,7 +430,13 @@ int launch_wave(const GcmKeyDev* key, const tg_batch& b, hipStream_t s) {
 // of ``order`` (first: NULL = 0, else a device count -- the key-table plan
 // puts the long records, which the octet kernel takes, in front); a record
 // whose key_idx is not below nkeys is skipped (open: status 0).
-constexpr int kTvThreads = 768;
+#ifndef TG_TV_G
+#define TG_TV_G 1   // blocks per step (A/B builds, tools/build_variant.sh -DTG_TV_G=n)
+#endif
+#ifndef TG_TV_THREADS
+#define TG_TV_THREADS 512
+#endif
+constexpr int kTvThreads = TG_TV_THREADS;
 constexpr int kTvLds = 65536 + 16 * kTvThreads;
 
 template <int NR, bool OPEN>
@@ -454,7 +460,7 @@ __global__ __launch_bounds__(kTvThreads) void gcm_table_vkernel(const GcmTableKe
     for (int k = 0; k < 4 * (NR + 1); ++k) rk.w[k] = kp->rk[k];
     const GhashClmul gh{*reinterpret_cast<const uint4*>(kp->hn)};
     const uint32_t lane4 = (threadIdx.x & 31u) << 2;
-    gcm_record<NR, OPEN, 1, RkRegs<NR>, GhashClmul, true>(b, i, lane4, rk, gh, 65536u + 16u * threadIdx.x);
+    gcm_record<NR, OPEN, TG_TV_G, RkRegs<NR>, GhashClmul, true>(b, i, lane4, rk, gh, 65536u + 16u * threadIdx.x);
 }
 
 template <int NR, bool OPEN>

@@ -157,6 +157,7 @@ struct SingleKeyCtx {   // one key for the batch: 8-bit H^8 tables in LDS (gmul_
     __device__ __forceinline__ uint4 gmul(uint4 y) const { return gmul_rot(y, threadIdx.x & 15u, jt); }
     // y * H^8 ^ x: Horner's step with the input folded into the XOR tree
     __device__ __forceinline__ uint4 gmulx(uint4 y, uint4 x) const { return gmul_rot(y, threadIdx.x & 15u, jt, x); }
+    __device__ __forceinline__ const uint4* masks() const { return nullptr; }
 };
 // SingleKeyCtx with the lane's offset row held in registers (the hybrid
 // kernel's waves of both roles: one ds_read_b128 fewer per block; T-table
@@ -168,12 +169,15 @@ struct SingleKeyRowCtx {
     __device__ __forceinline__ uint4 hpow(int e) const { return key->hpow[e - 1]; }
     __device__ __forceinline__ uint4 gmul(uint4 y) const { return gmul_rot_j(y, threadIdx.x & 15u, jw); }
     __device__ __forceinline__ uint4 gmulx(uint4 y, uint4 x) const { return gmul_rot_j(y, threadIdx.x & 15u, jw, x); }
+    __device__ __forceinline__ const uint4* masks() const { return nullptr; }
 };
 struct TableKeyCtx {    // a key of a key table: the wave's 4-bit H^8 tables in LDS (gmul4)
     const uint32_t* rkw;
     const uint4* hp;    // H^1 .. H^64 of this key (tg_launch_table_hpow)
     uint32_t tab;
+    const uint4* mt = nullptr;   // per plan slot E_K(J0) (kt_mask_kernel), or computed per record
     __device__ __forceinline__ const uint32_t* rk() const { return rkw; }
+    __device__ __forceinline__ const uint4* masks() const { return mt; }
     __device__ __forceinline__ uint4 hpow(int e) const { return hp[e - 1]; }
 #if defined(TG_KT_NO_GHASH)   // measurement build: no GHASH multiply (wrong tags)
     __device__ __forceinline__ uint4 gmul(uint4 y) const { return y; }
@@ -420,15 +424,22 @@ __device__ __forceinline__ void octet_job(const KC& kc, const tg_batch& b,
         y = kc.gmulx(y, make_uint4(bswap32((uint32_t)(abits >> 32)), bswap32((uint32_t)abits),
                                      bswap32((uint32_t)(cbits >> 32)), bswap32((uint32_t)cbits)));
     }
+    // E_K(J0) precomputed per plan slot (key tables: kt_mask_kernel), loaded
+    // here so the lift below covers the load
+    const uint4* mt = kc.masks();
+    uint4 mask = make_uint4(0, 0, 0, 0);
+    if (mt && valid) mask = gload16(reinterpret_cast<const uint8_t*>(mt + t));
     // lift by H^(LPR - l) and XOR-reduce over the record's lanes
     uint4 yn = norm4(y);
     if (yn.x | yn.y | yn.z | yn.w) yn = gf128_mul(yn, kc.hpow(LPR - l));
 #pragma unroll
     for (int m = 1; m < LPR; m <<= 1) yn = xor4(yn, shfl_xor4(yn, m));
     // tag = GHASH ^ E_K(J0), J0 = nonce || be32(1) (aesgcm.py:112-122)
-    if (valid) nv = load_partial(b.nonce + 12 * i, 12);   // reloaded: not held across the loop
-    const uint4 mask = TROLE ? aes_ctr<NR>(lane4, rkT, cc, 1u)
-                             : aes_block_sb<NR>(rk, make_uint4(nv.x, nv.y, nv.z, bswap32(1u)), sbox);
+    if (!mt) {
+        if (valid) nv = load_partial(b.nonce + 12 * i, 12);   // reloaded: not held across the loop
+        mask = TROLE ? aes_ctr<NR>(lane4, rkT, cc, 1u)
+                     : aes_block_sb<NR>(rk, make_uint4(nv.x, nv.y, nv.z, bswap32(1u)), sbox);
+    }
     const uint4 tag = xor4(norm4(yn), mask);
     const bool tag_aligned = aligned && tail == 0;
     if (!OPEN) {
@@ -705,7 +716,10 @@ constexpr uint32_t kKthSbox = 2 * 65536 + 3 * 8192;
 constexpr uint32_t kKthRec = kKthSbox + 256;
 constexpr uint32_t kKthRecArea = 384;                   // (64 / 32) x 128 + (64 / 32) x 64
 constexpr size_t kKthLds = kKthRec + kKthWaves * kKthRecArea;
-constexpr uint32_t kKthChunk = 4;
+#ifndef TG_KTH_CHUNK
+#define TG_KTH_CHUNK 2   // A/B builds (tools/build_variant.sh -DTG_KTH_CHUNK=n)
+#endif
+constexpr uint32_t kKthChunk = TG_KTH_CHUNK;
 constexpr int kKthTDefault = 7;
 static_assert(kKthLds <= 163840, "key-table hybrid LDS");
 
@@ -722,6 +736,7 @@ __global__ __launch_bounds__(kKthThreads) void gcm_kth_kernel(const GcmTableKey*
                                                              const uint32_t* __restrict__ jobpos,
                                                              const uint32_t* __restrict__ njobs_p,
                                                              const uint32_t* __restrict__ nlong_p,
+                                                             const uint4* __restrict__ masks,
                                                              uint32_t* __restrict__ queue, uint32_t nt) {
     stage_te(reinterpret_cast<uint32_t*>(g_lds_bs8) + kTeBase / 4);
     stage_sbox(kKthSbox);
@@ -754,7 +769,7 @@ __global__ __launch_bounds__(kKthThreads) void gcm_kth_kernel(const GcmTableKey*
             }
             tg_batch bj = b;
             bj.n = p1;   // the job's slots are p0 .. p1 - 1 (at most two)
-            const TableKeyCtx kc{keys[k].rk, hpow + 64u * k, tab};
+            const TableKeyCtx kc{keys[k].rk, hpow + 64u * k, tab, masks};
             const bs8::KeyPlanesVmemFolded km{{reinterpret_cast<const uint4*>(planes + kKtPlaneWords * k)}};
             if (wave < nt)
                 octet_job<NR, OPEN, true, bs8::KeyPlanesVmemFolded, TableKeyCtx, false, 32, RkTab>(
@@ -765,6 +780,26 @@ __global__ __launch_bounds__(kKthThreads) void gcm_kth_kernel(const GcmTableKey*
         }
         if (tail) break;
     }
+}
+
+// E_K(J0) of every long record of a key-table plan, by plan slot (slots
+// [0, nlong)): masks[t] = E_K(nonce || be32(1)) with the record's key
+// (aesgcm.py:112-115), one lane per record, the S-box staged in LDS.  The
+// key-table hybrid reads it at the end of each record instead of running a
+// dependent 10- or 14-round chain per record and wave.
+template <int NR>
+__global__ __launch_bounds__(256) void kt_mask_kernel(const GcmTableKey* __restrict__ keys, tg_batch b,
+                                                      const uint32_t* __restrict__ order,
+                                                      const uint32_t* __restrict__ nlong_p,
+                                                      uint4* __restrict__ masks) {
+    stage_sbox(0);
+    __syncthreads();
+    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= *nlong_p) return;
+    const uint32_t i = gld(order, t);
+    const uint4 nv = load_partial(b.nonce + 12 * (uint64_t)i, 12);
+    const uint4 m = aes_block_sb<NR>(keys[gld(b.key_idx, i)].rk, make_uint4(nv.x, nv.y, nv.z, bswap32(1u)), 0u);
+    gstore16(reinterpret_cast<uint8_t*>(masks + t), m);
 }
 
 // Per key, the T-table waves' rotated round keys: rot[16 k + r] = rotr8 of
@@ -809,14 +844,22 @@ __global__ void kt_planes_kernel(const GcmTableKey* __restrict__ keys, uint64_t 
 template <int NR, bool OPEN>
 int launch_kth(const GcmTableKey* keys, const uint4* hpow, const uint32_t* planes, const uint4* rot,
                const tg_batch& b, hipStream_t s, const uint32_t* order, const uint32_t* jobpos,
-               const uint32_t* njobs, const uint32_t* nlong, uint32_t* queue) {
+               const uint32_t* njobs, const uint32_t* nlong, uint32_t* queue, uint4* masks) {
     const int t = opt(kOptKtT);
     if (t < 0 || t > kKthWaves) return TG_EINVAL;
     const uint32_t nt = t ? (uint32_t)t : (uint32_t)kKthTDefault;
     if (lds_attr((const void*)gcm_kth_kernel<NR, OPEN>, (int)kKthLds)) return TG_EHIP;
     if (hipMemsetAsync(queue, 0, 4, s) != hipSuccess) return TG_EHIP;
+#if defined(TG_KTH_NO_MASK)   // A/B builds: every wave computes its records' masks
+    masks = nullptr;
+#else
+    const uint64_t mblocks = (b.n + 255) / 256;   // nlong <= n
+    if (mblocks > 0x7fffffffull) return TG_EINVAL;
+    hipLaunchKernelGGL((kt_mask_kernel<NR>), dim3((unsigned)mblocks), dim3(256), 256, s, keys, b, order, nlong,
+                       masks);
+#endif
     hipLaunchKernelGGL((gcm_kth_kernel<NR, OPEN>), dim3((unsigned)device_cus()), dim3(kKthThreads), kKthLds, s,
-                       keys, hpow, planes, rot, b, order, jobpos, njobs, nlong, queue, nt);
+                       keys, hpow, planes, rot, b, order, jobpos, njobs, nlong, masks, queue, nt);
     return hipGetLastError() == hipSuccess ? TG_OK : TG_EHIP;
 }
 
@@ -858,8 +901,11 @@ int launch_kt(const GcmTableKey* keys, uint64_t nkeys, const uint4* hpow, const 
                              nullptr, nullptr, nullptr, &plan, s);
     if (rc) return rc;
     const size_t so = (b.n * 4 + 255) & ~(size_t)255, sj = ((b.n + 1) * 4 + 255) & ~(size_t)255;
+    // the key-table hybrid's per-slot tag masks (kt_mask_kernel) after the plan
+    const size_t sm = hybrid && lpr == 32 ? b.n * 16 : 0;
+    const size_t po = (so + sj + 256 + plan + 255) & ~(size_t)255;
     uint8_t* buf = nullptr;
-    if (hipMallocAsync((void**)&buf, so + sj + 256 + plan, s) != hipSuccess) return TG_EHIP;
+    if (hipMallocAsync((void**)&buf, po + sm, s) != hipSuccess) return TG_EHIP;
     uint32_t* order = reinterpret_cast<uint32_t*>(buf);
     uint32_t* jobpos = reinterpret_cast<uint32_t*>(buf + so);
     uint32_t* njobs = reinterpret_cast<uint32_t*>(buf + so + sj);
@@ -875,7 +921,7 @@ int launch_kt(const GcmTableKey* keys, uint64_t nkeys, const uint4* hpow, const 
             case 16: rc = launch_kt_jobs<NR, OPEN, 16>(keys, nkeys, hpow, planes, b, s, order, jobpos, njobs, nlong); break;
             case 32:
                 rc = hybrid ? launch_kth<NR, OPEN>(keys, hpow, planes, rot, b, s, order, jobpos, njobs, nlong,
-                                                   njobs + 16)
+                                                   njobs + 16, reinterpret_cast<uint4*>(buf + po))
                             : launch_kt_jobs<NR, OPEN, 32>(keys, nkeys, hpow, planes, b, s, order, jobpos, njobs,
                                                            nlong);
                 break;
