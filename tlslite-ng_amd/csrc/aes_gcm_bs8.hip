@@ -165,11 +165,12 @@ struct SingleKeyCtx {   // one key for the batch: 8-bit H^8 tables in LDS (gmul_
 struct SingleKeyRowCtx {
     const GcmKeyDev* key;
     uint4 jw;
+    const uint4* mt = nullptr;   // per slot E_K(J0) (hy_mask_kernel), or computed per record
     __device__ __forceinline__ const uint32_t* rk() const { return key->rk; }
     __device__ __forceinline__ uint4 hpow(int e) const { return key->hpow[e - 1]; }
     __device__ __forceinline__ uint4 gmul(uint4 y) const { return gmul_rot_j(y, threadIdx.x & 15u, jw); }
     __device__ __forceinline__ uint4 gmulx(uint4 y, uint4 x) const { return gmul_rot_j(y, threadIdx.x & 15u, jw, x); }
-    __device__ __forceinline__ const uint4* masks() const { return nullptr; }
+    __device__ __forceinline__ const uint4* masks() const { return mt; }
 };
 struct TableKeyCtx {    // a key of a key table: the wave's 4-bit H^8 tables in LDS (gmul4)
     const uint32_t* rkw;
@@ -520,7 +521,8 @@ __global__ __launch_bounds__(THREADS) void gcm_hy_kernel(const GcmKeyDev* __rest
                                                             uint32_t* __restrict__ queue,
                                                             uint32_t nt, uint32_t prio,
                                                             const uint4* __restrict__ krows,
-                                                            const uint4* __restrict__ rkrot) {
+                                                            const uint4* __restrict__ rkrot,
+                                                            const uint4* __restrict__ masks) {
     stage_ghash_rot(g_lds_bs8, key->ghash8, kHyJt);
     stage_te(reinterpret_cast<uint32_t*>(g_lds_bs8) + kTeBase / 4);
     stage_sbox(kHySbox);
@@ -540,7 +542,7 @@ __global__ __launch_bounds__(THREADS) void gcm_hy_kernel(const GcmKeyDev* __rest
             if (job >= njobs) break;
             asm volatile("" ::: "memory");
             const tg_batch b = *bp;
-            octet_job<NR, OPEN, true>(SingleKeyRowCtx{key, jw}, b, order, 8ull * job, recw, rk,
+            octet_job<NR, OPEN, true>(SingleKeyRowCtx{key, jw, masks}, b, order, 8ull * job, recw, rk,
                                       kHySbox, bs8::KeyPlanesVmemFolded{{krows}});
         }
     } else {
@@ -557,7 +559,7 @@ __global__ __launch_bounds__(THREADS) void gcm_hy_kernel(const GcmKeyDev* __rest
             asm volatile("" ::: "memory");
             const tg_batch b = *bp;
             octet_job<NR, OPEN, false, bs8::KeyPlanesVmemFolded, SingleKeyRowCtx, (THREADS < 1024)>(
-                SingleKeyRowCtx{key, jw}, b, order, 8ull * job, recw, none, kHySbox,
+                SingleKeyRowCtx{key, jw, masks}, b, order, 8ull * job, recw, none, kHySbox,
                 bs8::KeyPlanesVmemFolded{{krows}});
         }
     }
@@ -572,25 +574,52 @@ __global__ void hy_setup_kernel(tg_batch b, uint32_t* queue, tg_batch* bcopy) {
     }
 }
 
-// The hybrid launch's 256 bytes of scratch (job counter, batch copy), one
-// buffer per (device, stream) for the life of the process: launches on one
-// stream are ordered, so they can share it, and launches on different streams
-// never do.  (Round 3 allocated it per launch with hipMallocAsync, and built
-// the key rows per launch in the setup kernel; both are gone from the
-// per-call path.)  A stream handle reused after hipStreamDestroy inherits the
-// buffer; the destroyed stream's work has completed by then.
-uint8_t* hy_scratch(hipStream_t s) {
+// E_K(J0) of every record of a single-key batch, by slot t (record order[t]
+// or t): one lane per record, round keys by scalar loads, S-box in LDS.  The
+// hybrid's waves read it at the end of each record instead of running a
+// dependent 10- or 14-round chain per job (aesgcm.py:112-115).
+template <int NR>
+__global__ __launch_bounds__(256) void hy_mask_kernel(const GcmKeyDev* __restrict__ key, tg_batch b,
+                                                      const uint32_t* __restrict__ order,
+                                                      uint4* __restrict__ masks) {
+    stage_sbox(0);
+    __syncthreads();
+    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= b.n) return;
+    const uint64_t i = order ? gld(order, t) : t;
+    const uint4 nv = load_partial(b.nonce + 12 * i, 12);
+    gstore16(reinterpret_cast<uint8_t*>(masks + t),
+             aes_block_sb<NR>(key->rk, make_uint4(nv.x, nv.y, nv.z, bswap32(1u)), 0u));
+}
+
+// The hybrid launch's scratch: job counter and batch copy (256 bytes), then
+// one 16-byte tag mask per record (hy_mask_kernel).  One buffer per (device,
+// stream) for the life of the process: launches on one stream are ordered,
+// so they can share it, and launches on different streams never do.  It grows
+// (stream-ordered free of the old one) when a batch needs more mask room.
+// (Round 3 allocated scratch per launch with hipMallocAsync, and built the key
+// rows per launch in the setup kernel; both are gone from the per-call path.)
+// A stream handle reused after hipStreamDestroy inherits the buffer; the
+// destroyed stream's work has completed by then.
+uint8_t* hy_scratch(hipStream_t s, uint64_t nrec) {
+    struct Buf {
+        uint8_t* p;
+        uint64_t cap;   // records of mask room
+    };
     static std::mutex mu;
-    static std::map<std::pair<int, hipStream_t>, uint8_t*> pool;
+    static std::map<std::pair<int, hipStream_t>, Buf> pool;
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess) return nullptr;
     std::lock_guard<std::mutex> g(mu);
     auto it = pool.find({dev, s});
-    if (it != pool.end()) return it->second;
+    if (it != pool.end() && it->second.cap >= nrec) return it->second.p;
+    uint64_t cap = it != pool.end() ? it->second.cap : 0;
+    cap = nrec > 2 * cap ? nrec : 2 * cap;
     uint8_t* p = nullptr;
-    if (hipMalloc((void**)&p, 256) != hipSuccess) return nullptr;
-    pool[{dev, s}] = p;
-    return p;
+    if (hipMallocAsync((void**)&p, 256 + 16 * cap, s) != hipSuccess) return nullptr;
+    const bool freed = it == pool.end() || hipFreeAsync(it->second.p, s) == hipSuccess;
+    pool[{dev, s}] = Buf{p, cap};
+    return freed ? p : nullptr;
 }
 
 template <int NR, bool OPEN>
@@ -622,20 +651,32 @@ int launch_hy(const GcmKeyDev* key, const tg_batch& b, hipStream_t s, const uint
     if (lds_attr(fn, (int)kHyLds)) return TG_EHIP;
     // job counter + batch copy: per-stream scratch (hy_scratch); the key rows
     // and rotated round keys come with the key (GcmKeyDev::bs8rows, rkrot)
-    uint8_t* scratch = hy_scratch(s);
+#if defined(TG_HY_NO_MASK)   // A/B builds: every wave computes its records' masks
+    uint8_t* scratch = hy_scratch(s, 0);
+    uint4* masks = nullptr;
+#else
+    uint8_t* scratch = hy_scratch(s, b.n);
+    uint4* masks = scratch ? reinterpret_cast<uint4*>(scratch + 256) : nullptr;
+#endif
     if (!scratch) return TG_EHIP;
     uint32_t* queue = reinterpret_cast<uint32_t*>(scratch);
     tg_batch* bcopy = reinterpret_cast<tg_batch*>(scratch + 64);
     hipLaunchKernelGGL(hy_setup_kernel, dim3(1), dim3(64), 0, s, b, queue, bcopy);
     if (hipGetLastError() != hipSuccess) return TG_EHIP;
+    if (masks && b.n) {
+        const uint64_t mblocks = (b.n + 255) / 256;
+        if (mblocks > 0x7fffffffull) return TG_EINVAL;
+        hipLaunchKernelGGL((hy_mask_kernel<NR>), dim3((unsigned)mblocks), dim3(256), 256, s, key, b, order, masks);
+        if (hipGetLastError() != hipSuccess) return TG_EHIP;
+    }
     const uint4* krows = reinterpret_cast<const uint4*>(key->bs8rows);
     const uint4* rkrot = reinterpret_cast<const uint4*>(key->rkrot);
     if (small)
         hipLaunchKernelGGL((gcm_hy_kernel<NR, OPEN, 768>), dim3((unsigned)device_cus()), dim3(768), kHyLds, s,
-                           key, (const tg_batch*)bcopy, order, queue, nt, prio, krows, rkrot);
+                           key, (const tg_batch*)bcopy, order, queue, nt, prio, krows, rkrot, masks);
     else
         hipLaunchKernelGGL((gcm_hy_kernel<NR, OPEN, 1024>), dim3((unsigned)device_cus()), dim3(1024), kHyLds,
-                           s, key, (const tg_batch*)bcopy, order, queue, nt, prio, krows, rkrot);
+                           s, key, (const tg_batch*)bcopy, order, queue, nt, prio, krows, rkrot, masks);
     return hipGetLastError() == hipSuccess ? TG_OK : TG_EHIP;
 }
 
