@@ -757,10 +757,7 @@ constexpr uint32_t kKthSbox = 2 * 65536 + 3 * 8192;
 constexpr uint32_t kKthRec = kKthSbox + 256;
 constexpr uint32_t kKthRecArea = 384;                   // (64 / 32) x 128 + (64 / 32) x 64
 constexpr size_t kKthLds = kKthRec + kKthWaves * kKthRecArea;
-#ifndef TG_KTH_CHUNK
-#define TG_KTH_CHUNK 2   // A/B builds (tools/build_variant.sh -DTG_KTH_CHUNK=n)
-#endif
-constexpr uint32_t kKthChunk = TG_KTH_CHUNK;
+constexpr uint32_t kKthChunk = 2;   // jobs per grab (1 / 2 / 4 / 8: 607 / 614 / 610 / 590 GiB/s, profiles/r04/r4j)
 constexpr int kKthTDefault = 7;
 static_assert(kKthLds <= 163840, "key-table hybrid LDS");
 
@@ -778,6 +775,7 @@ __global__ __launch_bounds__(kKthThreads) void gcm_kth_kernel(const GcmTableKey*
                                                              const uint32_t* __restrict__ njobs_p,
                                                              const uint32_t* __restrict__ nlong_p,
                                                              const uint4* __restrict__ masks,
+                                                             const uint32_t* __restrict__ jobkey,
                                                              uint32_t* __restrict__ queue, uint32_t nt) {
     stage_te(reinterpret_cast<uint32_t*>(g_lds_bs8) + kTeBase / 4);
     stage_sbox(kKthSbox);
@@ -792,19 +790,30 @@ __global__ __launch_bounds__(kKthThreads) void gcm_kth_kernel(const GcmTableKey*
         j0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)j0);
         if (j0 >= njobs) break;
         const uint32_t j1 = j0 + kKthChunk < njobs ? j0 + kKthChunk : njobs;
+        // the chunk's job bounds and keys in one round of loads (jobkey:
+        // kth_jobkey_kernel), not a dependent jobpos -> order -> key_idx
+        // chain per job
+        // (chunk of two: the values by selects, so the loop body -- both
+        // roles' code -- exists once)
+        const uint32_t pa = gld(jobpos, j0), pb = gld(jobpos, j0 + 1u),
+                       pc = j0 + 2u <= njobs ? gld(jobpos, j0 + 2u) : 0u;
+        const uint32_t ka = gld(jobkey, j0), kb = j0 + 1u < njobs ? gld(jobkey, j0 + 1u) : 0u;
         bool tail = false;
-        for (uint32_t job = j0; job < j1; ++job) {
-            const uint32_t p0 = gld(jobpos, job), p1 = gld(jobpos, job + 1);
+        for (uint32_t q = 0; q < j1 - j0; ++q) {
+            const uint32_t p0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)(q ? pb : pa));
+            const uint32_t p1 = (uint32_t)__builtin_amdgcn_readfirstlane((int)(q ? pc : pb));
             // the plan's tail (slots >= nlong) is the lane kernel's, and every
             // later job lies in it too
             if (p0 >= nlong) {
                 tail = true;
                 break;
             }
-            const uint32_t k = (uint32_t)__builtin_amdgcn_readfirstlane((int)gld(b.key_idx, gld(order, p0)));
+            const uint32_t k = (uint32_t)__builtin_amdgcn_readfirstlane((int)(q ? kb : ka));
             if (k != cur) {
                 __builtin_amdgcn_wave_barrier();   // the previous job's lookups are done
+#if !defined(TG_KT_NO_BUILD)   // measurement build: tables left as they are (wrong tags)
                 build_table4(tab, hpow[64u * k + 31u]);
+#endif
                 cur = k;
                 __builtin_amdgcn_wave_barrier();
             }
@@ -841,6 +850,18 @@ __global__ __launch_bounds__(256) void kt_mask_kernel(const GcmTableKey* __restr
     const uint4 nv = load_partial(b.nonce + 12 * (uint64_t)i, 12);
     const uint4 m = aes_block_sb<NR>(keys[gld(b.key_idx, i)].rk, make_uint4(nv.x, nv.y, nv.z, bswap32(1u)), 0u);
     gstore16(reinterpret_cast<uint8_t*>(masks + t), m);
+}
+
+// Per job of a key-table plan, the key of its records (the plan groups a
+// job's records by key): jobkey[j] = key_idx[order[jobpos[j]]] for the long
+// jobs (jobpos[j] < nlong); tail jobs are never read.
+__global__ void kth_jobkey_kernel(const uint32_t* __restrict__ jobpos, const uint32_t* __restrict__ njobs_p,
+                                  const uint32_t* __restrict__ nlong_p, const uint32_t* __restrict__ order,
+                                  const uint32_t* __restrict__ key_idx, uint32_t* __restrict__ jobkey) {
+    const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= *njobs_p) return;
+    const uint32_t p0 = jobpos[j];
+    jobkey[j] = p0 < *nlong_p ? key_idx[order[p0]] : 0xffffffffu;
 }
 
 // Per key, the T-table waves' rotated round keys: rot[16 k + r] = rotr8 of
@@ -885,7 +906,8 @@ __global__ void kt_planes_kernel(const GcmTableKey* __restrict__ keys, uint64_t 
 template <int NR, bool OPEN>
 int launch_kth(const GcmTableKey* keys, const uint4* hpow, const uint32_t* planes, const uint4* rot,
                const tg_batch& b, hipStream_t s, const uint32_t* order, const uint32_t* jobpos,
-               const uint32_t* njobs, const uint32_t* nlong, uint32_t* queue, uint4* masks) {
+               const uint32_t* njobs, const uint32_t* nlong, uint32_t* queue, uint4* masks,
+               uint32_t* jobkey) {
     const int t = opt(kOptKtT);
     if (t < 0 || t > kKthWaves) return TG_EINVAL;
     const uint32_t nt = t ? (uint32_t)t : (uint32_t)kKthTDefault;
@@ -899,8 +921,11 @@ int launch_kth(const GcmTableKey* keys, const uint4* hpow, const uint32_t* plane
     hipLaunchKernelGGL((kt_mask_kernel<NR>), dim3((unsigned)mblocks), dim3(256), 256, s, keys, b, order, nlong,
                        masks);
 #endif
+    // every job holds at least one plan slot, so njobs <= n
+    hipLaunchKernelGGL(kth_jobkey_kernel, dim3((unsigned)((b.n + 256) / 256)), dim3(256), 0, s, jobpos, njobs,
+                       nlong, order, b.key_idx, jobkey);
     hipLaunchKernelGGL((gcm_kth_kernel<NR, OPEN>), dim3((unsigned)device_cus()), dim3(kKthThreads), kKthLds, s,
-                       keys, hpow, planes, rot, b, order, jobpos, njobs, nlong, masks, queue, nt);
+                       keys, hpow, planes, rot, b, order, jobpos, njobs, nlong, masks, jobkey, queue, nt);
     return hipGetLastError() == hipSuccess ? TG_OK : TG_EHIP;
 }
 
@@ -943,7 +968,7 @@ int launch_kt(const GcmTableKey* keys, uint64_t nkeys, const uint4* hpow, const 
     if (rc) return rc;
     const size_t so = (b.n * 4 + 255) & ~(size_t)255, sj = ((b.n + 1) * 4 + 255) & ~(size_t)255;
     // the key-table hybrid's per-slot tag masks (kt_mask_kernel) after the plan
-    const size_t sm = hybrid && lpr == 32 ? b.n * 16 : 0;
+    const size_t sm = hybrid && lpr == 32 ? b.n * 16 + (b.n + 1) * 4 : 0;   // + kth_jobkey_kernel's keys
     const size_t po = (so + sj + 256 + plan + 255) & ~(size_t)255;
     uint8_t* buf = nullptr;
     if (hipMallocAsync((void**)&buf, po + sm, s) != hipSuccess) return TG_EHIP;
@@ -962,7 +987,8 @@ int launch_kt(const GcmTableKey* keys, uint64_t nkeys, const uint4* hpow, const 
             case 16: rc = launch_kt_jobs<NR, OPEN, 16>(keys, nkeys, hpow, planes, b, s, order, jobpos, njobs, nlong); break;
             case 32:
                 rc = hybrid ? launch_kth<NR, OPEN>(keys, hpow, planes, rot, b, s, order, jobpos, njobs, nlong,
-                                                   njobs + 16, reinterpret_cast<uint4*>(buf + po))
+                                                   njobs + 16, reinterpret_cast<uint4*>(buf + po),
+                                                   reinterpret_cast<uint32_t*>(buf + po + b.n * 16))
                             : launch_kt_jobs<NR, OPEN, 32>(keys, nkeys, hpow, planes, b, s, order, jobpos, njobs,
                                                            nlong);
                 break;
