@@ -266,6 +266,9 @@ __device__ __forceinline__ void octet_job(const KC& kc, const tg_batch& b,
     // batches in which every valid lane of the wave has all eight blocks full
     // (any alignment: the fast path's accesses are gload16u / gstore16u)
     const uint32_t nfast = wave_min_u32(valid ? nfl >> 3 : 0xffffffffu);
+    // per-slot precomputed keystream blocks: E_K(J0) at 2 t, the last block's
+    // at 2 t + 1 when the record's last batch holds only that block
+    const uint4* mt = kc.masks();
 
     // GHASH over this lane's AAD positions (aesgcm.py:69-79), zero-padded blocks
     uint4 y = make_uint4(0, 0, 0, 0);
@@ -340,7 +343,16 @@ __device__ __forceinline__ void octet_job(const KC& kc, const tg_batch& b,
         // bitsliced waves: in the open kernel the extra path's registers
         // spill elsewhere and cost 2 % (profiles/r02/v66_one_block/).
         const bool one = !OPEN && __all(!valid || nvl <= 8u * beta + 1u);
-        if (TROLE) {
+        // the same batch when its one block per lane is the record's last and
+        // the launch precomputed that block's keystream (mask kernels, slot
+        // 2 t + 1): no cipher at all, either role.  Seal only: in the open
+        // kernel the path cost registers (spills) and time
+        // (profiles/r04/r4p/).
+        if (!OPEN && mt && __all(!valid || nvl <= 8u * beta || (nvl == 8u * beta + 1u && blk0 == nc - 1u))) {
+            uint4 ks[1] = {rkl};
+            if (valid && nvl == 8u * beta + 1u) ks[0] = xor4(gload16(reinterpret_cast<const uint8_t*>(mt + 2 * t + 1)), rkl);
+            consume(ks, blk0, 0, std::integral_constant<int, 1>(), nullptr);
+        } else if (TROLE) {
             // through the 256-counter window cache when no lane of the wave
             // crosses a window in this batch (wave-uniform); two halves of four.
             // Octets: one window for the batch's counters c0 .. c0 + 56; pairs
@@ -425,11 +437,10 @@ __device__ __forceinline__ void octet_job(const KC& kc, const tg_batch& b,
         y = kc.gmulx(y, make_uint4(bswap32((uint32_t)(abits >> 32)), bswap32((uint32_t)abits),
                                      bswap32((uint32_t)(cbits >> 32)), bswap32((uint32_t)cbits)));
     }
-    // E_K(J0) precomputed per plan slot (key tables: kt_mask_kernel), loaded
-    // here so the lift below covers the load
-    const uint4* mt = kc.masks();
+    // E_K(J0) precomputed per slot (slot 2 t; hy_mask_kernel, kt_mask_kernel),
+    // loaded here so the lift below covers the load
     uint4 mask = make_uint4(0, 0, 0, 0);
-    if (mt && valid) mask = gload16(reinterpret_cast<const uint8_t*>(mt + t));
+    if (mt && valid) mask = gload16(reinterpret_cast<const uint8_t*>(mt + 2 * t));
     // lift by H^(LPR - l) and XOR-reduce over the record's lanes
     uint4 yn = norm4(y);
     if (yn.x | yn.y | yn.z | yn.w) yn = gf128_mul(yn, kc.hpow(LPR - l));
@@ -588,12 +599,19 @@ __global__ __launch_bounds__(256) void hy_mask_kernel(const GcmKeyDev* __restric
     if (t >= b.n) return;
     const uint64_t i = order ? gld(order, t) : t;
     const uint4 nv = load_partial(b.nonce + 12 * i, 12);
-    gstore16(reinterpret_cast<uint8_t*>(masks + t),
+    gstore16(reinterpret_cast<uint8_t*>(masks + 2 * t),
              aes_block_sb<NR>(key->rk, make_uint4(nv.x, nv.y, nv.z, bswap32(1u)), 0u));
+    // a record whose last batch row (8 x 8 blocks) holds one block -- a full
+    // TLS 1.3 record's 16 385-byte inner plaintext -- gets that block's
+    // keystream too (counter 2 + nc - 1, octet_job's tail path)
+    const uint32_t nc = (rec_len(b, i) + 15) >> 4;
+    if (nc % 64u == 1u)
+        gstore16(reinterpret_cast<uint8_t*>(masks + 2 * t + 1),
+                 aes_block_sb<NR>(key->rk, make_uint4(nv.x, nv.y, nv.z, bswap32(nc + 1u)), 0u));
 }
 
 // The hybrid launch's scratch: job counter and batch copy (256 bytes), then
-// one 16-byte tag mask per record (hy_mask_kernel).  One buffer per (device,
+// two 16-byte keystream blocks per record (hy_mask_kernel).  One buffer per (device,
 // stream) for the life of the process: launches on one stream are ordered,
 // so they can share it, and launches on different streams never do.  It grows
 // (stream-ordered free of the old one) when a batch needs more mask room.
@@ -616,7 +634,7 @@ uint8_t* hy_scratch(hipStream_t s, uint64_t nrec) {
     uint64_t cap = it != pool.end() ? it->second.cap : 0;
     cap = nrec > 2 * cap ? nrec : 2 * cap;
     uint8_t* p = nullptr;
-    if (hipMallocAsync((void**)&p, 256 + 16 * cap, s) != hipSuccess) return nullptr;
+    if (hipMallocAsync((void**)&p, 256 + 32 * cap, s) != hipSuccess) return nullptr;
     const bool freed = it == pool.end() || hipFreeAsync(it->second.p, s) == hipSuccess;
     pool[{dev, s}] = Buf{p, cap};
     return freed ? p : nullptr;
@@ -848,8 +866,14 @@ __global__ __launch_bounds__(256) void kt_mask_kernel(const GcmTableKey* __restr
     if (t >= *nlong_p) return;
     const uint32_t i = gld(order, t);
     const uint4 nv = load_partial(b.nonce + 12 * (uint64_t)i, 12);
-    const uint4 m = aes_block_sb<NR>(keys[gld(b.key_idx, i)].rk, make_uint4(nv.x, nv.y, nv.z, bswap32(1u)), 0u);
-    gstore16(reinterpret_cast<uint8_t*>(masks + t), m);
+    const uint32_t* rk = keys[gld(b.key_idx, i)].rk;
+    gstore16(reinterpret_cast<uint8_t*>(masks + 2 * t), aes_block_sb<NR>(rk, make_uint4(nv.x, nv.y, nv.z, bswap32(1u)), 0u));
+    // a record whose last batch row (8 x 32 blocks) holds one block: that
+    // block's keystream, counter 2 + nc - 1 (octet_job's tail path)
+    const uint32_t nc = (rec_len(b, i) + 15) >> 4;
+    if (nc % 256u == 1u)
+        gstore16(reinterpret_cast<uint8_t*>(masks + 2 * t + 1),
+                 aes_block_sb<NR>(rk, make_uint4(nv.x, nv.y, nv.z, bswap32(nc + 1u)), 0u));
 }
 
 // Per job of a key-table plan, the key of its records (the plan groups a
@@ -968,7 +992,7 @@ int launch_kt(const GcmTableKey* keys, uint64_t nkeys, const uint4* hpow, const 
     if (rc) return rc;
     const size_t so = (b.n * 4 + 255) & ~(size_t)255, sj = ((b.n + 1) * 4 + 255) & ~(size_t)255;
     // the key-table hybrid's per-slot tag masks (kt_mask_kernel) after the plan
-    const size_t sm = hybrid && lpr == 32 ? b.n * 16 + (b.n + 1) * 4 : 0;   // + kth_jobkey_kernel's keys
+    const size_t sm = hybrid && lpr == 32 ? b.n * 32 + (b.n + 1) * 4 : 0;   // + kth_jobkey_kernel's keys
     const size_t po = (so + sj + 256 + plan + 255) & ~(size_t)255;
     uint8_t* buf = nullptr;
     if (hipMallocAsync((void**)&buf, po + sm, s) != hipSuccess) return TG_EHIP;
@@ -988,7 +1012,7 @@ int launch_kt(const GcmTableKey* keys, uint64_t nkeys, const uint4* hpow, const 
             case 32:
                 rc = hybrid ? launch_kth<NR, OPEN>(keys, hpow, planes, rot, b, s, order, jobpos, njobs, nlong,
                                                    njobs + 16, reinterpret_cast<uint4*>(buf + po),
-                                                   reinterpret_cast<uint32_t*>(buf + po + b.n * 16))
+                                                   reinterpret_cast<uint32_t*>(buf + po + b.n * 32))
                             : launch_kt_jobs<NR, OPEN, 32>(keys, nkeys, hpow, planes, b, s, order, jobpos, njobs,
                                                            nlong);
                 break;
