@@ -488,6 +488,10 @@ def measured_traffic(path, kernel, n, L):
             "write_size_bytes": round(k["write_size_bytes"]), "access_shape": k["shape"],
             "fetch_factor": k["fetch_factor"], "write_factor": k["write_factor"],
             "traffic_over_algorithmic": round(k["hbm_bytes"] / algorithmic_bytes(n, L, kernel.rsplit("_", 1)[1]), 3),
+            # the launch's other kernel (AES-GCM: hy_mask_kernel, round 4), not in hbm_bytes
+            "mask_kernel_bytes": (round(t["kernels"]["aes128gcm_masks"]["hbm_bytes"])
+                                  if kernel.startswith("aes128gcm") and "aes128gcm_masks" in t.get("kernels", {})
+                                  else None),
             "source": os.path.relpath(path, ROOT)}
 
 
@@ -502,9 +506,14 @@ def c4_traffic(path, op):
     parts = [ks.get("c4_kt_" + op), ks.get("c4_lane_" + op)]
     if not all(parts):
         return None
-    return {"hbm_bytes": round(sum(k["hbm_bytes"] for k in parts)),
-            "kernels": {"long_records (gcm_kth_kernel)": round(parts[0]["hbm_bytes"]),
-                        "gcm_table_vkernel": round(parts[1]["hbm_bytes"])},
+    kernels = {"long_records (gcm_kth_kernel)": round(parts[0]["hbm_bytes"]),
+               "gcm_table_vkernel": round(parts[1]["hbm_bytes"])}
+    # the per-record keystream precompute and per-job keys (round 4), one
+    # launch each per seal or open, when the summary has them
+    for lab, name in (("c4_masks", "kt_mask_kernel"), ("c4_jobkey", "kth_jobkey_kernel")):
+        if ks.get(lab):
+            kernels[name] = round(ks[lab]["hbm_bytes"])
+    return {"hbm_bytes": sum(kernels.values()), "kernels": kernels,
             "source": os.path.relpath(path, ROOT)}
 
 

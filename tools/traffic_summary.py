@@ -19,6 +19,9 @@ factors of its shape:
                       long records), whole-line layout -> the octet factors
   c4_lane_*           gcm_table_vkernel (config 4's short records), 16 B per
                       lane, one record per lane -> the lane factors
+  aes128gcm_masks,    hy_mask_kernel, kt_mask_kernel, kth_jobkey_kernel: one
+  c4_masks, c4_jobkey lane per record (or job), launched with every seal and
+                      open (labels are per launch) -> the lane factors
   c5_prep, c5_seal    config 5 (bench.py --config c5, collected from its own
                       passes): seal_prep (one thread per record: header,
                       inner type, nonce / AAD rows -> the lane factors) and
@@ -54,7 +57,12 @@ KERNELS = [(r"gcm_hy_kernel<10, false", "aes128gcm_seal", "octet", "octet"),
            (r"gcm_kth_kernel<14, false", "c4_kt_seal", "octet", "octet"),
            (r"gcm_kth_kernel<14, true", "c4_kt_open", "octet", "octet"),
            (r"gcm_table_vkernel<14, false", "c4_lane_seal", "lane", "lane"),
-           (r"gcm_table_vkernel<14, true", "c4_lane_open", "lane", "lane")]
+           (r"gcm_table_vkernel<14, true", "c4_lane_open", "lane", "lane"),
+           # round 4: the per-record keystream precomputes launched with each
+           # seal and open (one lane per record: the lane factors)
+           (r"hy_mask_kernel<10>", "aes128gcm_masks", "lane", "lane"),
+           (r"kt_mask_kernel<14>", "c4_masks", "lane", "lane"),
+           (r"kth_jobkey_kernel", "c4_jobkey", "lane", "lane")]
 KERNELS_C5 = [(r"seal_prep", "c5_prep", "lane", "lane"),
               (r"gcm_hy_kernel<10, false", "c5_seal", "octet", "octet")]
 
