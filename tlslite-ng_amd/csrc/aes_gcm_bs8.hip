@@ -614,7 +614,9 @@ __global__ __launch_bounds__(256) void hy_mask_kernel(const GcmKeyDev* __restric
 // two 16-byte keystream blocks per record (hy_mask_kernel).  One buffer per (device,
 // stream) for the life of the process: launches on one stream are ordered,
 // so they can share it, and launches on different streams never do.  It grows
-// (stream-ordered free of the old one) when a batch needs more mask room.
+// (at least doubling) when a batch needs more mask room; the outgrown buffer
+// is kept, not freed, because another host thread launching on the same
+// stream may already hold it (its launches stay stream-ordered with ours).
 // (Round 3 allocated scratch per launch with hipMallocAsync, and built the key
 // rows per launch in the setup kernel; both are gone from the per-call path.)
 // A stream handle reused after hipStreamDestroy inherits the buffer; the
@@ -634,10 +636,9 @@ uint8_t* hy_scratch(hipStream_t s, uint64_t nrec) {
     uint64_t cap = it != pool.end() ? it->second.cap : 0;
     cap = nrec > 2 * cap ? nrec : 2 * cap;
     uint8_t* p = nullptr;
-    if (hipMallocAsync((void**)&p, 256 + 32 * cap, s) != hipSuccess) return nullptr;
-    const bool freed = it == pool.end() || hipFreeAsync(it->second.p, s) == hipSuccess;
+    if (hipMalloc((void**)&p, 256 + 32 * cap) != hipSuccess) return nullptr;
     pool[{dev, s}] = Buf{p, cap};
-    return freed ? p : nullptr;
+    return p;
 }
 
 template <int NR, bool OPEN>
