@@ -257,14 +257,15 @@ def main():
                          "roofline.traffic")
     ap.add_argument("--record-align", type=int, default=128,
                     help="byte alignment of each sealed record (ct||tag) in the packed batch")
-    ap.add_argument("--config", default="headline", choices=["headline", "c1", "c4", "c5", "ingest"],
+    ap.add_argument("--config", default="headline", choices=["headline", "c1", "c4", "c5", "ingest", "ccm"],
                     help="headline = BASELINE configs[1]+[2] (the metric); c1 = configs[0] "
                          "(4096 x 1 KiB ChaCha20-Poly1305, the device path beside the host CPU "
                          "run in full); c4 = configs[3] "
                          "(AES-256-GCM, 65536 keys, Zipf lengths); c5 = configs[4] (TLS 1.3 "
                          "AES-128-GCM record seal through the framing path, seq-sharded); "
                          "ingest = the host ingest pipeline (tlsgpu.ingest, SURVEY 8(f) row 3), "
-                         "host memory to host memory")
+                         "host memory to host memory; ccm = AES-128-CCM and CCM_8 seal/open "
+                         "(SURVEY 8(f) row 2) at the headline's record shape")
     ap.add_argument("--dist-selftest", action="store_true",
                     help="create the process group even at world size 1 (TLSGPU_DIST_SELFTEST=1) "
                          "so the counter reduction and the rate gather run through the backend "
@@ -281,7 +282,7 @@ def main():
         # N ranks, one process per GPU, started here before anything in this
         # process touches the GPU; this process only waits and passes on the
         # ranks' exit status (rank 0 prints the JSON line)
-        if args.config in ("c1", "c4", "ingest"):
+        if args.config in ("c1", "c4", "ingest", "ccm"):
             ap.error("--config %s runs on one GPU (BASELINE configs[3] / the host pipeline)" % args.config)
         backend = os.environ.get("TLSGPU_DIST_BACKEND", "nccl")
         if backend == "nccl":
@@ -310,6 +311,8 @@ def main():
         return run_config4(args)
     if args.config == "c5":
         return run_config5(args)
+    if args.config == "ccm":
+        return run_ccm(args)
 
     import torch
     import torch.distributed as dist
@@ -805,6 +808,114 @@ def run_config5(args):
     if tgd.group_active(dist):
         dist.destroy_process_group()
     if not ok:
+        sys.exit(3)
+
+
+def run_ccm(args):
+    """SURVEY 8(f) row 2 (aesccm.py:11-155): AES-128-CCM and AES-128-CCM_8
+    seal + open of ``--records`` TLS 1.3 records of ``--len`` bytes (default
+    the headline's 2^20 x 16 KiB), single key, records resident in HBM, one
+    GPU.  Not a BASELINE config (the reference publishes no CCM figure); the
+    row measures the CCM kernels at the headline's shape.  Checked untimed:
+    every record opens back (status and plaintext), and 64 sampled sealed
+    records equal the C oracle's AESCCM restatement byte for byte.  CPU
+    baseline: the C oracle's batch entry (the restatement, threaded) on the
+    usable cores over a bounded sample."""
+    import numpy as np
+    import torch
+    import tlsgpu
+    from vectors import tls13_aad
+    from tlsgpu import distributed as tgd
+    sys.path.insert(0, ROOT)
+    from oracle import oracle as O
+    torch.cuda.set_device(int(os.environ.get("LOCAL_RANK", "0")))
+    n, L = args.records, args.len
+    SLc = (L + TAG_LEN + args.record_align - 1) // args.record_align * args.record_align
+    g = torch.Generator(device="cuda").manual_seed(0x7715)
+    inp = torch.randint(0, 256, (n * L,), dtype=torch.uint8, device="cuda", generator=g)
+    sealed = torch.empty(n * SLc, dtype=torch.uint8, device="cuda")
+    back = torch.empty(n * L, dtype=torch.uint8, device="cuda")
+    nonces = torch.empty(NONCE_LEN * n, dtype=torch.uint8, device="cuda")
+    aad = torch.tensor(list(tls13_aad(L)), dtype=torch.uint8, device="cuda")
+    hrng = torch.Generator().manual_seed(0x7716)
+    iv = bytes(torch.randint(0, 256, (12,), dtype=torch.uint8, generator=hrng).tolist())
+    key = bytes(torch.randint(0, 256, (16,), dtype=torch.uint8, generator=hrng).tolist())
+    tgd.shard_nonces(tlsgpu, iv, 0, n, nonces)
+    stream = torch.cuda.current_stream()
+    per_op, ok, total_ms, mism = {}, True, 0.0, 0
+    for tl, name in ((16, "aes128ccm"), (8, "aes128ccm_8")):
+        c = tlsgpu.HipAESCCM(bytearray(key), tag_length=tl)
+        status = torch.zeros(n, dtype=torch.uint8, device="cuda")
+        seal_b = tlsgpu.make_batch(n, inp, sealed, nonces, aad=aad, fixed_len=L, in_stride=L,
+                                   out_stride=SLc, fixed_aad_len=AAD_LEN)
+        open_b = tlsgpu.make_batch(n, sealed, back, nonces, aad=aad, fixed_len=L, in_stride=SLc,
+                                   out_stride=L, fixed_aad_len=AAD_LEN, status=status)
+        ev = {"seal": [], "open": []}
+        for it in range(args.warmup + args.steps):
+            for op, fn, bt in (("seal", tlsgpu.seal_batch, seal_b), ("open", tlsgpu.open_batch, open_b)):
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record(stream)
+                fn(c, bt, stream)
+                e1.record(stream)
+                if it >= args.warmup:
+                    ev[op].append((e0, e1))
+        torch.cuda.synchronize()
+        good = int(status.sum().item()) == n and bool(torch.equal(back, inp))
+        pick = sorted(set(list(range(0, n, max(1, n // 63)))[:63] + [n - 1]))
+        for i in pick:
+            nonce = tgd.tls13_nonces(iv, i, 1)
+            want = O.ccm_seal(key, nonce, inp[i * L:(i + 1) * L].cpu().numpy().tobytes(),
+                              bytes(tls13_aad(L)), taglen=tl)
+            got = sealed[i * SLc:i * SLc + L + tl].cpu().numpy().tobytes()
+            mism += int(bytes(want) != got)
+        ok = ok and good
+        for op in ("seal", "open"):
+            ms = sum(a.elapsed_time(b) for a, b in ev[op]) / len(ev[op])
+            total_ms += ms
+            alg = 2 * L + AAD_LEN + NONCE_LEN + tl
+            per_op["%s_%s" % (name, op)] = {
+                "ms": round(ms, 3), "payload_GiBps": round(n * L / (ms / 1e3) / 2 ** 30, 1),
+                "algorithmic_GBps": round(n * alg / (ms / 1e3) / 1e9, 1),
+                "frac": round(n * alg / (ms / 1e3) / 1e9 / HBM_PEAK_GBS, 4)}
+    dom = max(per_op, key=lambda k: per_op[k]["ms"])
+    line = {
+        "metric": "GiB/s device-resident record seal/open, AES-128-CCM + AES-128-CCM_8 %d B" % L,
+        "value": round(4 * n * L / (total_ms / 1e3) / 2 ** 30, 2), "unit": "GiB/s", "n_gpus": 1,
+        "steps": args.steps, "warmup": args.warmup, "higher_is_better": True, "scaling": "none",
+        "dtype": "u8", "data": "synthetic (torch.randint payloads)",
+        "config": {"workload": "SURVEY 8(f) row 2: %d x %d B TLS 1.3 records, single key, "
+                               "AES-128-CCM and CCM_8, seal+open (not a BASELINE config)" % (n, L),
+                   "records": n, "record_len": L, "sealed_stride": SLc},
+        "per_op": per_op,
+        "roofline": {"bound": "hbm", "kernel": dom, "achieved": per_op[dom]["algorithmic_GBps"],
+                     "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": per_op[dom]["frac"], "traffic": None},
+        "oracle_checked_records": 2 * len(pick), "oracle_mismatches": mism,
+        "verified": bool(ok and mism == 0)}
+    if not args.no_cpu_baseline:
+        cores = args.cpu_cores or host_cores()[0]
+        m = 4096 if n >= 4096 else n
+        x = inp[:m * L].view(m, L).cpu().numpy()
+        keys = np.frombuffer(key, np.uint8).reshape(1, 16)
+        nn = np.frombuffer(b"".join(tgd.tls13_nonces(iv, i, 1) for i in range(m)), np.uint8)
+        ad = np.frombuffer(bytes(tls13_aad(L)) * m, np.uint8)
+        obuf = np.zeros(m * (L + TAG_LEN), np.uint8)   # reused: no page faults in the timed loop
+        t0, reps = time.perf_counter(), 0
+        while True:
+            O.batch("aesccm", "seal", keys, nn, ad, np.arange(m, dtype=np.uint64) * AAD_LEN,
+                    np.full(m, AAD_LEN, np.uint32), x.reshape(-1), np.arange(m, dtype=np.uint64) * L,
+                    np.full(m, L, np.uint32), m * (L + TAG_LEN),
+                    np.arange(m, dtype=np.uint64) * (L + TAG_LEN), nthreads=cores, out=obuf)
+            reps += 1
+            if time.perf_counter() - t0 >= args.cpu_seconds:
+                break
+        dt = time.perf_counter() - t0
+        line["cpu_baseline"] = {"value": reps * m * L / dt / 2 ** 30, "unit": "GiB/s", "cores": cores,
+                                "kind": "port",
+                                "sample": "AES-128-CCM seal of %d x %d B records, repeated for %.1f s, "
+                                          "oracle/aead_oracle.c (the C restatement of aesccm.py) "
+                                          "threaded over %d cores" % (m, L, dt, cores)}
+    emit(line)
+    if not line["verified"]:
         sys.exit(3)
 
 

@@ -67,7 +67,7 @@ def test_nccl_needs_a_gpu_per_rank():
     assert "needs one GPU per rank, 0 visible" in r.stderr
 
 
-@pytest.mark.parametrize("config", ["c4", "ingest"])
+@pytest.mark.parametrize("config", ["c4", "ingest", "ccm", "c1"])
 def test_single_gpu_configs_refuse_n(config):
     r = _run(["--gpus", "2", "--config", config])
     assert r.returncode == 2 and "runs on one GPU" in r.stderr
