@@ -586,28 +586,36 @@ __global__ void hy_setup_kernel(tg_batch b, uint32_t* queue, tg_batch* bcopy) {
 }
 
 // E_K(J0) of every record of a single-key batch, by slot t (record order[t]
-// or t): one lane per record, round keys by scalar loads, S-box in LDS.  The
-// hybrid's waves read it at the end of each record instead of running a
-// dependent 10- or 14-round chain per job (aesgcm.py:112-115).
+// or t): a persistent grid of one 1024-thread workgroup per CU, the Te0/Te2
+// copies staged once per CU and the round keys in SGPRs, each lane a record
+// at a time with the T-table cipher (aes_block).  The hybrid's waves read it
+// at the end of each record instead of running a dependent 10- or 14-round
+// chain per job (aesgcm.py:112-115).  (A lane per record with the byte-wise
+// S-box cipher took 36 us per 2^20 records, profiles/r04/f2/.)
 template <int NR>
-__global__ __launch_bounds__(256) void hy_mask_kernel(const GcmKeyDev* __restrict__ key, tg_batch b,
-                                                      const uint32_t* __restrict__ order,
-                                                      uint4* __restrict__ masks) {
-    stage_sbox(0);
+__global__ __launch_bounds__(1024) void hy_mask_kernel(const GcmKeyDev* __restrict__ key, tg_batch b,
+                                                       const uint32_t* __restrict__ order,
+                                                       uint4* __restrict__ masks) {
+    stage_te(reinterpret_cast<uint32_t*>(g_lds_bs8));
+    RkRegs<NR> rk;
+#pragma unroll
+    for (int k = 0; k < 4 * (NR + 1); ++k) rk.w[k] = key->rk[k];
     __syncthreads();
-    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= b.n) return;
-    const uint64_t i = order ? gld(order, t) : t;
-    const uint4 nv = load_partial(b.nonce + 12 * i, 12);
-    gstore16(reinterpret_cast<uint8_t*>(masks + 2 * t),
-             aes_block_sb<NR>(key->rk, make_uint4(nv.x, nv.y, nv.z, bswap32(1u)), 0u));
-    // a record whose last batch row (8 x 8 blocks) holds one block -- a full
-    // TLS 1.3 record's 16 385-byte inner plaintext -- gets that block's
-    // keystream too (counter 2 + nc - 1, octet_job's tail path)
-    const uint32_t nc = (rec_len(b, i) + 15) >> 4;
-    if (nc % 64u == 1u)
-        gstore16(reinterpret_cast<uint8_t*>(masks + 2 * t + 1),
-                 aes_block_sb<NR>(key->rk, make_uint4(nv.x, nv.y, nv.z, bswap32(nc + 1u)), 0u));
+    const uint32_t lane4 = (threadIdx.x & 31u) << 2;   // Te block at LDS 0
+    for (uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; t < b.n;
+         t += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t i = order ? gld(order, t) : t;
+        const uint4 nv = load_partial(b.nonce + 12 * i, 12);
+        gstore16(reinterpret_cast<uint8_t*>(masks + 2 * t),
+                 aes_block<NR>(lane4, rk, make_uint4(nv.x, nv.y, nv.z, bswap32(1u))));
+        // a record whose last batch row (8 x 8 blocks) holds one block -- a
+        // full TLS 1.3 record's 16 385-byte inner plaintext -- gets that
+        // block's keystream too (counter 2 + nc - 1, octet_job's tail path)
+        const uint32_t nc = (rec_len(b, i) + 15) >> 4;
+        if (nc % 64u == 1u)
+            gstore16(reinterpret_cast<uint8_t*>(masks + 2 * t + 1),
+                     aes_block<NR>(lane4, rk, make_uint4(nv.x, nv.y, nv.z, bswap32(nc + 1u))));
+    }
 }
 
 // The hybrid launch's scratch: job counter and batch copy (256 bytes), then
@@ -683,9 +691,10 @@ int launch_hy(const GcmKeyDev* key, const tg_batch& b, hipStream_t s, const uint
     hipLaunchKernelGGL(hy_setup_kernel, dim3(1), dim3(64), 0, s, b, queue, bcopy);
     if (hipGetLastError() != hipSuccess) return TG_EHIP;
     if (masks && b.n) {
-        const uint64_t mblocks = (b.n + 255) / 256;
-        if (mblocks > 0x7fffffffull) return TG_EINVAL;
-        hipLaunchKernelGGL((hy_mask_kernel<NR>), dim3((unsigned)mblocks), dim3(256), 256, s, key, b, order, masks);
+        if (lds_attr((const void*)hy_mask_kernel<NR>, 65536)) return TG_EHIP;
+        const uint64_t wgs = (b.n + 1023) / 1024, cus = (uint64_t)device_cus();
+        const unsigned grid = (unsigned)(wgs < cus ? wgs : cus);   // persistent: at most one per CU
+        hipLaunchKernelGGL((hy_mask_kernel<NR>), dim3(grid), dim3(1024), 65536, s, key, b, order, masks);
         if (hipGetLastError() != hipSuccess) return TG_EHIP;
     }
     const uint4* krows = reinterpret_cast<const uint4*>(key->bs8rows);
