@@ -214,6 +214,13 @@ constexpr uint64_t kPlanMinRecords = 2049;
 // Key-table AES-GCM: records of at least this many bytes take the
 // key-grouped octet kernel, shorter ones the lane kernel (option kt_split).
 constexpr uint32_t kKtSplitDefault = 2048;
+// Small key-table batches -- at most this many records, or one length with
+// at most this many bytes in all -- run one record per wavefront (the wave
+// kernel, table-free GHASH, no plan): 0.014 / 0.023 / 0.099 ms for 1 / 2 048 /
+// 16 384 records of 1 KiB against 0.23 / 0.32 / 0.34 ms planned, and 0.11
+// against 0.21 ms for 2 048 records of 16 KiB (profiles/r04/r4w/).
+constexpr uint64_t kKtWaveMaxRecords = 2048;
+constexpr uint64_t kKtWaveMaxBytes = 16ull << 20;
 
 int launch_kernels(tg_key* k, const tg_batch& b, bool open, hipStream_t s, const uint32_t* order) {
     if (k->alg == TG_AES_GCM)
@@ -221,7 +228,8 @@ int launch_kernels(tg_key* k, const tg_batch& b, bool open, hipStream_t s, const
     return tg_launch_chacha(static_cast<const tg::ChachaKeyDev*>(k->dev_key), k->nkeys, b, open, s, order);
 }
 
-// Key-table AES-GCM (option gcm_table_variant): 0 = auto (length split at
+// Key-table AES-GCM (option gcm_table_variant): 0 = auto (small batches one
+// record per wavefront, see kKtWaveMaxRecords; otherwise a length split at
 // kt_split: the long records on the kernel kt_lpr picks -- 0 = default,
 // 8 / 16 / 32 / 64 lanes per record on the key-grouped bitsliced kernel, -1
 // the wave-per-record T-table kernel with 4-bit GHASH tables -- the rest on
@@ -240,6 +248,10 @@ int launch_gcm_table(tg_key* k, const tg_batch& b, bool open, hipStream_t s) {
         case 0: {
             const int sp = tg::opt(tg::kOptKtSplit);
             split = sp > 0 ? (uint32_t)sp : kKtSplitDefault;
+            // small batches (unless the split or the long-record kernel is forced)
+            if (sp == 0 && o == 0 &&
+                (b.n <= kKtWaveMaxRecords || (!b.len && b.n * (uint64_t)b.fixed_len <= kKtWaveMaxBytes)))
+                return tg_launch_gcm_table_wave(keys, k->nkeys, table_hpow(k), k->rounds, b, open, s, false);
             break;
         }
         case 1: split = 0xffffffffu; break;
@@ -248,6 +260,12 @@ int launch_gcm_table(tg_key* k, const tg_batch& b, bool open, hipStream_t s) {
         case 14: split = 0; lpr = 8; break;
         default: return TG_EINVAL;
     }
+    // One length for every record, below the split (or option no_plan): every
+    // record is the lane kernel's and a length order is moot, so no plan --
+    // its sort, scans and stream-ordered allocation are pure latency for small
+    // multi-session batches (profiles/r04/r4w/).
+    if (split != 0 && ((!b.len && b.fixed_len < split) || tg::opt(tg::kOptNoPlan)))
+        return tg_launch_gcm_table_lane(keys, k->nkeys, k->rounds, b, open, s, nullptr, nullptr);
     // the long records (lpr 32) on the T-table + bitsliced kernel unless
     // kt_hybrid = -1 (the bitsliced-only key-grouped kernel)
     const bool hybrid = lpr == 32 && tg::opt(tg::kOptKtHybrid) >= 0;
