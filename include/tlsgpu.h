@@ -63,7 +63,9 @@ int tg_init(int device);                   /* hipSetDevice for the calling threa
  * environment variable, read once at first use:
  *   gcm_variant        0 auto, 6 wave per record, 14 bitsliced octet,
  *                      15 hybrid octet, 16 T-table lane per record
- *   gcm_table_variant  0 auto (length split), 1 lane, 5 wave per record,
+ *   gcm_table_variant  0 auto (<= 2048 records, or one length with <= 16 MiB
+ *                      in all: wave per record without a plan; else the
+ *                      length split), 1 lane, 5 wave per record,
  *                      6 wave per record with 4-bit GHASH tables,
  *                      14 key-grouped octet
  *   kt_split           key-table length split in bytes (0 = 2048)
