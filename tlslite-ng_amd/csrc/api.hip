@@ -281,8 +281,9 @@ int launch(tg_key* k, const tg_batch& b, bool open, hipStream_t s) {
         return tg_launch_ccm(static_cast<const tg::AesKeyDev*>(k->dev_key), k->nkeys, k->rounds, k->taglen,
                              b, open, s);
     if (k->alg == TG_AES_GCM && k->nkeys > 1) return launch_gcm_table(k, b, open, s);
-    const bool wave = k->nkeys == 1 && ((k->alg == TG_AES_GCM && tg_gcm_wave_path(b.n)) ||
-                                        (k->alg == TG_CHACHA20_POLY1305 && tg_chacha_wave_path(b.n)));
+    // (ChaCha key tables take the wave kernel too: chacha_wave_kernel<.., MULTIKEY>)
+    const bool wave = (k->nkeys == 1 && k->alg == TG_AES_GCM && tg_gcm_wave_path(b.n)) ||
+                      (k->alg == TG_CHACHA20_POLY1305 && tg_chacha_wave_path(b.n));
     if (!b.len || b.n < kPlanMinRecords || wave || b.n > 0xffffffffull || tg::opt(tg::kOptNoPlan))
         return launch_kernels(k, b, open, s, nullptr);
     size_t scratch = 0;

@@ -486,9 +486,11 @@ __global__ __launch_bounds__(kChachaThreads, MINW) void chacha_kernel(
 template <int W>
 constexpr int chacha_wave_threads() { return W == 16 ? 1024 : 256; }
 
-template <bool OPEN, int W>
+// MULTIKEY: a key table (record i uses keys[key_idx[i]]; an index not below
+// nkeys skips the record, open status 0 -- the record group exits together).
+template <bool OPEN, int W, bool MULTIKEY>
 __global__ __launch_bounds__(chacha_wave_threads<W>()) void chacha_wave_kernel(
-    const ChachaKeyDev* __restrict__ keys, tg_batch b) {
+    const ChachaKeyDev* __restrict__ keys, uint64_t nkeys, tg_batch b) {
     constexpr uint32_t S = 64u * W;            // segments (threads) per record
     __shared__ F5 s_part[W];
     __shared__ uint32_t s_diff;
@@ -496,9 +498,18 @@ __global__ __launch_bounds__(chacha_wave_threads<W>()) void chacha_wave_kernel(
                        (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x / S));   // wave-uniform
     if (i >= b.n) return;   // whole record group (uniform)
     const uint32_t lane = threadIdx.x & (S - 1u);
+    const ChachaKeyDev* kp = keys;
+    if (MULTIKEY) {
+        const uint32_t ki = (uint32_t)__builtin_amdgcn_readfirstlane((int)gld(b.key_idx, i));
+        if (ki >= nkeys) {   // uniform over the record group
+            if (OPEN && b.status && lane == 0) b.status[i] = 0;
+            return;
+        }
+        kp = keys + ki;
+    }
     uint32_t k[8];
 #pragma unroll
-    for (int w = 0; w < 8; ++w) k[w] = keys->k[w];
+    for (int w = 0; w < 8; ++w) k[w] = kp->k[w];
     const uint8_t* in = rec_in(b, i);
     uint8_t* out = rec_out(b, i);
     const uint32_t len = rec_len(b, i);
@@ -619,21 +630,21 @@ template <bool OPEN, bool MULTIKEY>
 int launch(const ChachaKeyDev* keys, uint64_t nkeys, const tg_batch& b, hipStream_t s, const uint32_t* order) {
     const int v = opt(kOptChachaVariant);
     if (v != 0 && v != 3 && v != 4 && v != 5) return TG_EINVAL;
-    if (!MULTIKEY && wave_path(b.n)) {
+    if (wave_path(b.n)) {
         // waves per record as in the GCM launcher (aes_gcm.hip waves_per_record)
         const int o = opt(kOptWavesPerRecord);
         const int w = o ? o : b.n <= 512 ? 4 : 1;   // profiles/r01/v21_smallbatch.txt
         const uint64_t groups = w == 1 ? (b.n + 3) / 4 : b.n;
         if (groups > 0x7fffffffull) return TG_EINVAL;
         if (w == 16)
-            hipLaunchKernelGGL((chacha_wave_kernel<OPEN, 16>), dim3((unsigned)groups), dim3(1024), 0,
-                               s, keys, b);
+            hipLaunchKernelGGL((chacha_wave_kernel<OPEN, 16, MULTIKEY>), dim3((unsigned)groups), dim3(1024), 0,
+                               s, keys, nkeys, b);
         else if (w == 4)
-            hipLaunchKernelGGL((chacha_wave_kernel<OPEN, 4>), dim3((unsigned)groups), dim3(256), 0, s,
-                               keys, b);
+            hipLaunchKernelGGL((chacha_wave_kernel<OPEN, 4, MULTIKEY>), dim3((unsigned)groups), dim3(256), 0, s,
+                               keys, nkeys, b);
         else if (w == 1)
-            hipLaunchKernelGGL((chacha_wave_kernel<OPEN, 1>), dim3((unsigned)groups), dim3(256), 0, s,
-                               keys, b);
+            hipLaunchKernelGGL((chacha_wave_kernel<OPEN, 1, MULTIKEY>), dim3((unsigned)groups), dim3(256), 0, s,
+                               keys, nkeys, b);
         else
             return TG_EINVAL;
         return hipGetLastError() == hipSuccess ? TG_OK : TG_EHIP;

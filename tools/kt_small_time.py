@@ -23,13 +23,14 @@ def main():
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--len", type=int, default=1024)
     ap.add_argument("--max-records", type=int, default=65536)
+    ap.add_argument("--alg", default="aesgcm", choices=["aesgcm", "chacha20-poly1305"])
     args = ap.parse_args()
     import torch
     import tlsgpu
     from vectors import tls13_aad
     L, so = args.len, (args.len + 16 + 15) // 16 * 16
-    keys = [bytes([k]) * 16 for k in range(64)]
-    kt = tlsgpu.KeyTable("aesgcm", keys)
+    keys = [bytes([k]) * (16 if args.alg == "aesgcm" else 32) for k in range(64)]
+    kt = tlsgpu.KeyTable(args.alg, keys)
     stream = torch.cuda.current_stream()
     out = []
     for n in [m for m in (1, 16, 256, 2048, 8192, 16384, 65536) if m <= args.max_records]:
@@ -44,11 +45,15 @@ def main():
         kidx = torch.randint(0, 64, (n,), dtype=torch.int32, device="cuda", generator=g)
         lens = torch.full((n,), L, dtype=torch.int32, device="cuda")
         row = {"records": n, "len": L}
-        for mode, fixed, opts in (("auto, one length", True, {}), ("auto, length array", False, {}),
-                                  ("lane kernel after the plan (variant 1, length array)", False,
-                                   {"gcm_table_variant": 1}),
-                                  ("wave kernel, table-free GHASH (variant 5)", True, {"gcm_table_variant": 5}),
-                                  ("wave kernel, 4-bit tables (variant 6)", True, {"gcm_table_variant": 6})):
+        modes = ((("auto, one length", True, {}), ("auto, length array", False, {}),
+                  ("lane kernel after the plan (variant 1, length array)", False, {"gcm_table_variant": 1}),
+                  ("wave kernel, table-free GHASH (variant 5)", True, {"gcm_table_variant": 5}),
+                  ("wave kernel, 4-bit tables (variant 6)", True, {"gcm_table_variant": 6}))
+                 if args.alg == "aesgcm" else
+                 (("auto, one length", True, {}), ("auto, length array", False, {}),
+                  ("lane kernel (chacha_variant 5)", False, {"chacha_variant": 5}),
+                  ("wave kernel (chacha_variant 3)", True, {"chacha_variant": 3})))
+        for mode, fixed, opts in modes:
             kw = {"fixed_len": L} if fixed else {"lens": lens}
             sb = tlsgpu.make_batch(n, inp, sealed, nonces, aad=aad, in_stride=L, out_stride=so,
                                    fixed_aad_len=5, key_idx=kidx, **kw)
