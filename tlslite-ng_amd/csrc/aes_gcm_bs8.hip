@@ -861,29 +861,42 @@ __global__ __launch_bounds__(kKthThreads) void gcm_kth_kernel(const GcmTableKey*
 }
 
 // E_K(J0) of every long record of a key-table plan, by plan slot (slots
-// [0, nlong)): masks[t] = E_K(nonce || be32(1)) with the record's key
-// (aesgcm.py:112-115), one lane per record, the S-box staged in LDS.  The
+// [0, nlong)): masks[2 t] = E_K(nonce || be32(1)) with the record's key
+// (aesgcm.py:112-115).  A persistent grid of one 1024-thread workgroup per CU
+// (the Te0/Te2 copies staged once per CU), each lane a record at a time with
+// its key's round keys in VGPRs and the T-table cipher (aes_block).  The
 // key-table hybrid reads it at the end of each record instead of running a
-// dependent 10- or 14-round chain per record and wave.
+// dependent 10- or 14-round chain per record and wave.  (A lane per record
+// with the byte-wise S-box cipher took 49 us per config-4 launch.)
 template <int NR>
-__global__ __launch_bounds__(256) void kt_mask_kernel(const GcmTableKey* __restrict__ keys, tg_batch b,
-                                                      const uint32_t* __restrict__ order,
-                                                      const uint32_t* __restrict__ nlong_p,
-                                                      uint4* __restrict__ masks) {
-    stage_sbox(0);
+__global__ __launch_bounds__(1024) void kt_mask_kernel(const GcmTableKey* __restrict__ keys, tg_batch b,
+                                                       const uint32_t* __restrict__ order,
+                                                       const uint32_t* __restrict__ nlong_p,
+                                                       uint4* __restrict__ masks) {
+    stage_te(reinterpret_cast<uint32_t*>(g_lds_bs8));
     __syncthreads();
-    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= *nlong_p) return;
-    const uint32_t i = gld(order, t);
-    const uint4 nv = load_partial(b.nonce + 12 * (uint64_t)i, 12);
-    const uint32_t* rk = keys[gld(b.key_idx, i)].rk;
-    gstore16(reinterpret_cast<uint8_t*>(masks + 2 * t), aes_block_sb<NR>(rk, make_uint4(nv.x, nv.y, nv.z, bswap32(1u)), 0u));
-    // a record whose last batch row (8 x 32 blocks) holds one block: that
-    // block's keystream, counter 2 + nc - 1 (octet_job's tail path)
-    const uint32_t nc = (rec_len(b, i) + 15) >> 4;
-    if (nc % 256u == 1u)
-        gstore16(reinterpret_cast<uint8_t*>(masks + 2 * t + 1),
-                 aes_block_sb<NR>(rk, make_uint4(nv.x, nv.y, nv.z, bswap32(nc + 1u)), 0u));
+    const uint32_t lane4 = (threadIdx.x & 31u) << 2;   // Te block at LDS 0
+    const uint64_t nlong = *nlong_p;
+    for (uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; t < nlong;
+         t += (uint64_t)gridDim.x * blockDim.x) {
+        const uint32_t i = gld(order, t);
+        const uint4 nv = load_partial(b.nonce + 12 * (uint64_t)i, 12);
+        const uint4* kr = reinterpret_cast<const uint4*>(keys[gld(b.key_idx, i)].rk);
+        RkRegs<NR> rk;   // this record's key: per-lane values
+#pragma unroll
+        for (int q = 0; q <= NR; ++q) {
+            const uint4 v = gload16(reinterpret_cast<const uint8_t*>(kr + q));
+            rk.w[4 * q] = v.x; rk.w[4 * q + 1] = v.y; rk.w[4 * q + 2] = v.z; rk.w[4 * q + 3] = v.w;
+        }
+        gstore16(reinterpret_cast<uint8_t*>(masks + 2 * t),
+                 aes_block<NR>(lane4, rk, make_uint4(nv.x, nv.y, nv.z, bswap32(1u))));
+        // a record whose last batch row (8 x 32 blocks) holds one block: that
+        // block's keystream, counter 2 + nc - 1 (octet_job's tail path)
+        const uint32_t nc = (rec_len(b, i) + 15) >> 4;
+        if (nc % 256u == 1u)
+            gstore16(reinterpret_cast<uint8_t*>(masks + 2 * t + 1),
+                     aes_block<NR>(lane4, rk, make_uint4(nv.x, nv.y, nv.z, bswap32(nc + 1u))));
+    }
 }
 
 // Per job of a key-table plan, the key of its records (the plan groups a
@@ -950,10 +963,10 @@ int launch_kth(const GcmTableKey* keys, const uint4* hpow, const uint32_t* plane
 #if defined(TG_KTH_NO_MASK)   // A/B builds: every wave computes its records' masks
     masks = nullptr;
 #else
-    const uint64_t mblocks = (b.n + 255) / 256;   // nlong <= n
-    if (mblocks > 0x7fffffffull) return TG_EINVAL;
-    hipLaunchKernelGGL((kt_mask_kernel<NR>), dim3((unsigned)mblocks), dim3(256), 256, s, keys, b, order, nlong,
-                       masks);
+    if (lds_attr((const void*)kt_mask_kernel<NR>, 65536)) return TG_EHIP;
+    const uint64_t wgs = (b.n + 1023) / 1024, cus = (uint64_t)device_cus();   // nlong <= n
+    hipLaunchKernelGGL((kt_mask_kernel<NR>), dim3((unsigned)(wgs < cus ? wgs : cus)), dim3(1024), 65536, s, keys,
+                       b, order, nlong, masks);
 #endif
     // every job holds at least one plan slot, so njobs <= n
     hipLaunchKernelGGL(kth_jobkey_kernel, dim3((unsigned)((b.n + 256) / 256)), dim3(256), 0, s, jobpos, njobs,
