@@ -141,6 +141,54 @@ def cpu_baseline(L, cores, seconds, gpu_samples):
             "gpu_records_rechecked": len(gpu_samples), "gpu_records_match": bool(match)}
 
 
+# ------------------------------------------- per-rank checks (every N)
+
+def headline_check(samples):
+    """Every rank's own sampled records (alg, key, nonce, plaintext, aad, GPU
+    output) re-sealed with the C oracle (oracle/aead_oracle.c, pinned to the
+    reference's vectors): the number of records whose bytes differ."""
+    sys.path.insert(0, ROOT)
+    from oracle import oracle as O
+    bad = 0
+    for alg, key, nonce, pt, aad, got in samples:
+        seal = O.gcm_seal if alg.startswith("aes") else O.chacha_seal
+        bad += int(bytes(seal(key, nonce, pt, aad)) != bytes(got))
+    return bad
+
+
+def corrupt_for_test(samples, rank, field):
+    """Test hook (tests/test_bench_verify.py): TLSGPU_BENCH_CORRUPT_RANK=r
+    flips one byte of the first sample's GPU bytes on rank r before the
+    oracle check, so a one-shard failure must surface in the reduced
+    ``verified``.  ``field`` indexes the GPU bytes in a sample tuple."""
+    if not samples or os.environ.get("TLSGPU_BENCH_CORRUPT_RANK") != str(rank):
+        return samples
+    s0 = list(samples[0])
+    b = bytearray(s0[field])
+    b[len(b) // 2] ^= 0x01
+    s0[field] = bytes(b)
+    return [tuple(s0)] + list(samples[1:])
+
+
+def verify_shards(torch, dist, local_ok, bad, checked, device=None):
+    """The line's verification over ALL ranks (tlsgpu.distributed.
+    reduce_verification): MIN of each rank's own round-trip flag and oracle
+    agreement, SUM of the oracle mismatches and of the records checked.
+    Every rank returns the same (ok, mismatches, checked)."""
+    from tlsgpu import distributed as tgd
+    return tgd.reduce_verification(torch, dist, bool(local_ok) and bad == 0, bad, checked, device=device)
+
+
+def finish(dist, ok):
+    """Tear down the process group; exit 3 on every rank when any shard
+    failed its checks."""
+    from tlsgpu import distributed as tgd
+    if tgd.group_active(dist):
+        dist.destroy_process_group()
+    if not ok:
+        sys.exit(3)
+
+
 # ---------------------------------------------- BASELINE configs[0], in full
 
 C1_RECORDS, C1_LEN = 4096, 1024
@@ -390,7 +438,12 @@ def main():
             samples.append((a, keys[a], tgd.tls13_nonces(iv, first + i, 1),
                             inp[i * L:(i + 1) * L].cpu().numpy().tobytes(), bytes(tls13_aad(L)),
                             sealed[i * SL:i * SL + L + TAG_LEN].cpu().numpy().tobytes()))
-    ok = all(verified.values())
+    # every rank checks its own sampled records against the C oracle, and the
+    # line's verdict is reduced over all ranks (a wrong seq offset on rank g
+    # is symmetric in seal and open, so only the oracle sees it)
+    samples = corrupt_for_test(samples, rank, 5)
+    bad = headline_check(samples)
+    ok, bad_all, checked_all = verify_shards(torch, dist, all(verified.values()), bad, len(samples), device=dev)
     # the only collectives: counters summed, the timed span max-reduced and
     # the per-rank kernel times gathered (RCCL)
     sums, elapsed = tgd.reduce_counters(torch, dist, [n * args.steps * len(kinds),
@@ -449,7 +502,9 @@ def main():
                          "read_bytes_per_record": read_bytes(1, L, dom_op),
                          "algorithmic_bytes_per_launch": algorithmic_bytes(n, L, dom_op)},
             "verified": bool(ok),
-            "verified_per_cipher": verified,
+            "verified_scope": "all %d rank(s): MIN of each rank's round trip and oracle agreement" % world,
+            "verified_per_cipher_rank0": verified,
+            "oracle_checked_records": checked_all, "oracle_mismatches": bad_all,
             "auth_failures": int(sums[2]),
             "auth_failures_per_cipher": fails,
             "dist_backend": dist.get_backend() if tgd.group_active(dist) else None,
@@ -464,15 +519,14 @@ def main():
                                  for nm, ms in zip(names, r)} for r in rows]
         if e2e:
             line["end_to_end"] = e2e
-        if not args.no_cpu_baseline and world == 1:
+        if not args.no_cpu_baseline:
+            # rank 0 only, after the collectives, at any N (the other ranks
+            # go on to tear down their process group)
             cores = args.cpu_cores or host_cores()[0]
             line["cpu_baseline"] = cpu_baseline(L, cores, args.cpu_seconds, samples)
             line["cpu_baseline"]["config1"] = cpu_config1(cores)
         emit(line)
-    if tgd.group_active(dist):
-        dist.destroy_process_group()
-    if not ok:
-        sys.exit(3)
+    finish(dist, ok)
 
 
 def measured_traffic(path, kernel, n, L):
@@ -646,6 +700,57 @@ def cpu_baseline_c5(L, cores, seconds):
                       "of the reference path)" % (cores, seconds, L)}
 
 
+def _cpu_worker_c4(seed, seconds, start, q):
+    """Config 4's mix on one host process: AES-256-GCM sessions (a cipher
+    object per session, as RecordLayer keeps one per connection state,
+    recordlayer.py:1268-1323), Zipf(1.2) record lengths 64 B-16 KiB, TLS 1.2
+    nonce iv4 || seq and AAD seq || 0x17 0303 || len, seal then open with the
+    pure-Python restatement."""
+    sys.path.insert(0, ROOT)
+    import numpy as np
+    from oracle import pyaead
+    rng = np.random.default_rng(seed)
+    sessions = [(pyaead.AESGCM(rng.bytes(32)), rng.bytes(4)) for _ in range(16)]
+    lens = np.clip(64 * rng.zipf(1.2, 4096), 64, 16384)
+    data = rng.bytes(16384)
+    start.wait()
+    t0 = time.perf_counter()
+    done, i = 0, 0
+    while time.perf_counter() - t0 < seconds:
+        c, iv4 = sessions[i % len(sessions)]
+        L = int(lens[i % len(lens)])
+        seq = i.to_bytes(8, "big")
+        aad = seq + bytes([0x17, 3, 3, L >> 8, L & 0xff])
+        sealed = c.seal(iv4 + seq, data[:L], aad)
+        assert c.open(iv4 + seq, sealed, aad) == data[:L]
+        done += 2 * L
+        i += 1
+    q.put((done, time.perf_counter() - t0, i))
+
+
+def cpu_baseline_c4(cores, seconds):
+    """BASELINE configs[3] on the host cores: ``cores`` processes started
+    together, each sealing and opening config-4-shaped records (_cpu_worker_c4)
+    for ``seconds``; payload GiB/s counted like the GPU line (seal + open)."""
+    ctx = mp.get_context("spawn")
+    start, q = ctx.Barrier(cores + 1), ctx.Queue()
+    procs = [ctx.Process(target=_cpu_worker_c4, args=(3000 + c, seconds, start, q)) for c in range(cores)]
+    for p in procs:
+        p.start()
+    start.wait()
+    res = [q.get() for _ in procs]
+    for p in procs:
+        p.join()
+    total, wall, recs = sum(r[0] for r in res), max(r[1] for r in res), sum(r[2] for r in res)
+    cap, ncpu = host_cores()
+    return {"value": total / wall / 2 ** 30, "unit": "GiB/s", "cores": cores, "kind": "port",
+            "host_cpus": ncpu, "usable_cpus": cap,
+            "sample": "%d processes x %.0f s each (%d records in all), AES-256-GCM seal+open, 16 "
+                      "sessions per process, Zipf(1.2) lengths 64 B-16 KiB, TLS 1.2 nonce and AAD, "
+                      "oracle/pyaead.py (pure-Python restatement of the reference path)"
+                      % (cores, seconds, recs)}
+
+
 def run_config1(args):
     """BASELINE configs[0] (ChaCha20-Poly1305 seal + open of 4 096 x 1 KiB
     records, chacha20_poly1305.py:48,68): the device batch path, timed per
@@ -755,7 +860,7 @@ def run_config5(args):
     elapsed = tgd.timed(torch, dist, world, lambda s: step(True), args.steps)
     # untimed check: every wire record opens back to its fragment and type
     wl = int(wire_len[0].item())
-    samples = c5_samples(data, wire, wire_len, c5_pick(n), L) if rank == 0 else []
+    samples = c5_samples(data, wire, wire_len, c5_pick(n), L)   # every rank: its own shard
     back = torch.zeros(n * DS, dtype=torch.uint8, device="cuda")
     o_len = torch.zeros(n, dtype=torch.int32, device="cuda")
     o_ct = torch.zeros(n, dtype=torch.uint8, device="cuda")
@@ -768,14 +873,17 @@ def run_config5(args):
           bool(torch.equal(back.view(n, DS)[:, :L], orig)))
     hdr = wire[H:H + 5].cpu().numpy().tobytes()
     ok = ok and hdr == bytes([0x17, 0x03, 0x03, (L + 17) >> 8, (L + 17) & 0xff])
+    # each rank's 128 sampled wire records against the framing oracle at its
+    # own seq offset (first = g n), reduced over all ranks
+    bad = c5_check(corrupt_for_test(samples, rank, 2), key, iv, first)
+    ok, bad_all, checked_all = verify_shards(torch, dist, ok, bad, len(samples), device="cuda")
     sums, elapsed = tgd.reduce_counters(torch, dist, [n * args.steps, n * L * args.steps, 0],
                                         elapsed, device="cuda")
     dist_info = tgd.selftest_collectives(torch, dist, device="cuda") if tgd.group_active(dist) else None
     ms = sum(a.elapsed_time(b) for a, b in evs) / len(evs)
     ach = c5_algorithmic_bytes(n, L, "seal") / (ms / 1e3) / 1e9
+    rows = tgd.gather_rows(torch, dist, [ms, float(first)], device="cuda")
     if rank == 0:
-        bad = c5_check(samples, key, iv, first)
-        ok = ok and bad == 0
         line = {
             "metric": "GiB/s device-resident TLS 1.3 AES-128-GCM record seal (BASELINE configs[4])",
             "value": round(sums[1] / elapsed / 2 ** 30, 2), "unit": "GiB/s", "n_gpus": world,
@@ -792,23 +900,26 @@ def run_config5(args):
                          "frac_read": round(n * L / (ms / 1e3) / 1e9 / HBM_PEAK_GBS, 4),
                          "bytes_per_record": c5_algorithmic_bytes(1, L, "seal"), "traffic": None,
                          "ms": round(ms, 3)},
-            "oracle_checked_records": len(samples), "oracle_mismatches": bad,
+            "oracle_checked_records": checked_all, "oracle_mismatches": bad_all,
             "verified": bool(ok),
+            "verified_scope": "all %d rank(s): MIN of each rank's open-back check and its %d sampled "
+                              "wire records against the framing oracle" % (world, len(samples)),
             "dist_backend": dist.get_backend() if tgd.group_active(dist) else None}
+        if world > 1:
+            line["per_rank"] = [{"rank": g, "seq0": int(r[1]), "ms": round(r[0], 3),
+                                 "frac": round(c5_algorithmic_bytes(n, L, "seal") / (r[0] / 1e3) / 1e9 /
+                                               HBM_PEAK_GBS, 4)} for g, r in enumerate(rows)]
         if dist_info:
             line["dist_selftest"] = dist_info
         tr = c5_traffic(args.traffic_file, n, L) if world == 1 else None
         if tr:
             line["roofline"]["traffic"] = tr["hbm_bytes"]
             line["roofline"]["traffic_detail"] = tr
-        if not args.no_cpu_baseline and world == 1:
+        if not args.no_cpu_baseline:   # rank 0, after the collectives, at any N
             cores = args.cpu_cores or host_cores()[0]
             line["cpu_baseline"] = cpu_baseline_c5(L, cores, args.cpu_seconds)
         emit(line)
-    if tgd.group_active(dist):
-        dist.destroy_process_group()
-    if not ok:
-        sys.exit(3)
+    finish(dist, ok)
 
 
 def run_ccm(args):
@@ -980,6 +1091,18 @@ def run_config4(args):
             ms[op].append((e0, e1))
     torch.cuda.synchronize()
     ok = int(status.sum().item()) == n and torch.equal(back, inp)
+    # 64 sampled records (the first, the last, spread over the batch) re-sealed
+    # with the C oracle under their own session key
+    sys.path.insert(0, ROOT)
+    from oracle import oracle as O
+    mism, pick = 0, sorted(set(list(range(0, n, max(1, n // 62)))[:62] + [n - 1]))
+    for i in pick:
+        L_i = int(lens[i])
+        pt = inp[int(in_off[i]):int(in_off[i]) + L_i].cpu().numpy().tobytes()
+        got = sealed[int(out_off[i]):int(out_off[i]) + L_i + TAG_LEN].cpu().numpy().tobytes()
+        want = O.gcm_seal(bytes(keys[key_idx[i]]), bytes(nonce[i]), pt, bytes(aad[i]))
+        mism += int(bytes(want) != got)
+    ok = ok and mism == 0
     payload = float(lens.sum())
     res = {}
     for op, lst in ms.items():
@@ -1006,6 +1129,7 @@ def run_config4(args):
                          "achieved": res[dom]["algorithmic_GBps"], "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": res[dom]["frac"], "frac_read": res[dom]["frac_read"],
                          "traffic": None},
+            "oracle_checked_records": len(pick), "oracle_mismatches": mism,
             "verified": bool(ok)}
     tr = c4_traffic(args.traffic_file, dom) if n == 1 << 20 and not args.c4_presorted else None
     if tr:
@@ -1013,6 +1137,8 @@ def run_config4(args):
         tr["traffic_over_algorithmic"] = round(tr["hbm_bytes"] / alg, 3)
         line["roofline"]["traffic"] = tr["hbm_bytes"]
         line["roofline"]["traffic_detail"] = tr
+    if not args.no_cpu_baseline:
+        line["cpu_baseline"] = cpu_baseline_c4(args.cpu_cores or host_cores()[0], args.cpu_seconds)
     emit(line)
     if not ok:
         sys.exit(3)

@@ -162,3 +162,16 @@ def test_world1_group_selftest(tmp_path):
     mp.spawn(_world1_worker, args=(str(tmp_path),), nprocs=1, join=True)
     got = eval(open(tmp_path / "world1").read())   # noqa: S307 -- our own repr
     assert got == (True, "gloo", 1, [3.0, 4.0, 0.0], 1.5, [[7.0, 8.0]])
+
+
+def test_world2_without_master_addr_refused(monkeypatch):
+    """At world > 1 the free-port fallback would give every rank its own
+    port and hang the rendezvous: without MASTER_ADDR it is a
+    DistError before any process group is created."""
+    monkeypatch.setenv("WORLD_SIZE", "2")
+    monkeypatch.setenv("RANK", "1")
+    monkeypatch.setenv("LOCAL_RANK", "1")
+    monkeypatch.delenv("MASTER_ADDR", raising=False)
+    with pytest.raises(tgd.DistError, match="MASTER_ADDR"):
+        tgd.init_process(torch, dist, backend="gloo", use_gpu=False)
+    assert not dist.is_initialized()

@@ -192,7 +192,8 @@ def test_config1_digest(torch, tg):
 
 # ------------------------------------------- full-size (BASELINE configs 2/3)
 
-@pytest.mark.parametrize("alg", ["aesgcm", "chacha", "aesgcm-bs8", "chacha-regs"])
+@pytest.mark.parametrize("alg", ["aesgcm", "chacha", "aesgcm-bs8", "chacha-regs", "aesgcm-stride",
+                                 "chacha-stride"])
 def test_full_size_roundtrip_and_samples(torch, tg, oracle_mod, alg):
     """2^20 x 16 KiB records: every record's ciphertext and tag bit-exact
     against the threaded C oracle (tests/fullcheck.py, 2^16-record chunks),
@@ -200,16 +201,21 @@ def test_full_size_roundtrip_and_samples(torch, tg, oracle_mod, alg):
     through the oracle's per-record entry point.
     aesgcm-bs8 forces the 8-block bitsliced kernel (gcm_variant 14),
     chacha-regs the register-staged tile fill (chacha_variant 4; the default
-    fills it by LDS-DMA)."""
+    fills it by LDS-DMA).  *-stride: sealed records at bench.py's stride,
+    L + 16 rounded up to a 128-byte line (16 512 B), the layout the metric is
+    measured on."""
     variant = 14 if alg == "aesgcm-bs8" else 0
     cv = 4 if alg == "chacha-regs" else 0
-    alg = {"aesgcm-bs8": "aesgcm", "chacha-regs": "chacha"}.get(alg, alg)
+    stride = 16512 if alg.endswith("-stride") else None
+    alg = {"aesgcm-bs8": "aesgcm", "chacha-regs": "chacha", "aesgcm-stride": "aesgcm",
+           "chacha-stride": "chacha"}.get(alg, alg)
     with tg.options(gcm_variant=variant, chacha_variant=cv):
-        _full_size(torch, tg, oracle_mod, alg)
+        _full_size(torch, tg, oracle_mod, alg, stride)
 
 
-def _full_size(torch, tg, oracle_mod, alg):
+def _full_size(torch, tg, oracle_mod, alg, stride=None):
     n, L = 1 << 20, 16384
+    SL = stride or L + 16
     g = torch.Generator(device="cuda").manual_seed(0x7715)
     inp = torch.randint(0, 256, (n * L,), dtype=torch.uint8, device="cuda", generator=g)
     key = bytes(detbytes("full-size-" + alg, 16 if alg == "aesgcm" else 32))
@@ -218,13 +224,13 @@ def _full_size(torch, tg, oracle_mod, alg):
     nonces = torch.zeros(12 * n, dtype=torch.uint8, device="cuda")
     tg.make_nonces(iv, 0, n, nonces)
     aad = torch.tensor(list(tls13_aad(L)), dtype=torch.uint8, device="cuda")
-    sealed = torch.empty(n * (L + 16), dtype=torch.uint8, device="cuda")
+    sealed = torch.empty(n * SL, dtype=torch.uint8, device="cuda")
     tg.seal_batch(obj, tg.make_batch(n, inp, sealed, nonces, aad=aad, fixed_len=L, in_stride=L,
-                                     out_stride=L + 16, fixed_aad_len=5))
+                                     out_stride=SL, fixed_aad_len=5))
     back = torch.empty_like(inp)
     status = torch.zeros(n, dtype=torch.uint8, device="cuda")
     tg.open_batch(obj, tg.make_batch(n, sealed, back, nonces, aad=aad, fixed_len=L,
-                                     in_stride=L + 16, out_stride=L, fixed_aad_len=5,
+                                     in_stride=SL, out_stride=L, fixed_aad_len=5,
                                      status=status))
     torch.cuda.synchronize()
     assert int(status.sum()) == n
@@ -233,7 +239,7 @@ def _full_size(torch, tg, oracle_mod, alg):
     import fullcheck
     recs, nbytes = fullcheck.check_all(
         torch, oracle_mod, alg, np.frombuffer(key, np.uint8), inp, np.arange(n) * L,
-        np.full(n, L), sealed, np.arange(n) * (L + 16), fullcheck.tls13_nonces(iv, 0, n),
+        np.full(n, L), sealed, np.arange(n) * SL, fullcheck.tls13_nonces(iv, 0, n),
         np.frombuffer(bytes(tls13_aad(L)), np.uint8), np.zeros(n), np.full(n, 5))
     assert recs == n and nbytes == n * (L + 16)
     rng = np.random.default_rng(1)
@@ -244,7 +250,7 @@ def _full_size(torch, tg, oracle_mod, alg):
         nonce = bytes(tls13_nonce(iv, i))
         want = (oracle_mod.gcm_seal if alg == "aesgcm" else oracle_mod.chacha_seal)(
             key, nonce, pt, bytes(tls13_aad(L)))
-        got = sealed[i * (L + 16):(i + 1) * (L + 16)].cpu().numpy().tobytes()
+        got = sealed[i * SL:i * SL + L + 16].cpu().numpy().tobytes()
         assert got == bytes(want), i
     del inp, sealed
     torch.cuda.empty_cache()

@@ -1,0 +1,48 @@
+"""GPU: the per-launch scratch of the hybrid AES-GCM kernel (job counter,
+batch copy and the per-record keystream masks) is stream-ordered memory from
+the device pool, freed behind each launch: batches launched on
+many short-lived streams leave device memory flat, and their records stay
+right."""
+import numpy as np
+import pytest
+
+from vectors import tls13_aad
+
+pytestmark = pytest.mark.gpu
+
+
+def test_many_streams_memory_flat(oracle_mod):
+    import torch
+    import tlsgpu
+    import fullcheck
+    if not torch.cuda.is_available():
+        pytest.fail("GPU tests need a visible MI355X")
+    n, L = 32768, 256          # above the wave-kernel range: the hybrid kernel (1 MiB of masks)
+    key, iv = bytes(range(16)), bytes(range(40, 52))
+    obj = tlsgpu.HipAESGCM(bytearray(key))
+    g = torch.Generator(device="cuda").manual_seed(11)
+    inp = torch.randint(0, 256, (n * L,), dtype=torch.uint8, device="cuda", generator=g)
+    out = torch.zeros(n * (L + 16), dtype=torch.uint8, device="cuda")
+    nonces = torch.zeros(12 * n, dtype=torch.uint8, device="cuda")
+    tlsgpu.make_nonces(iv, 0, n, nonces)
+    aad = torch.tensor(list(tls13_aad(L)), dtype=torch.uint8, device="cuda")
+    b = tlsgpu.make_batch(n, inp, out, nonces, aad=aad, fixed_len=L, in_stride=L, out_stride=L + 16,
+                          fixed_aad_len=5)
+    s0 = torch.cuda.Stream()
+    tlsgpu.seal_batch(obj, b, s0)          # first use: the pool grows once
+    torch.cuda.synchronize()
+    free0 = torch.cuda.mem_get_info()[0]
+    for k in range(48):                    # a new stream per batch, dropped after it
+        s = torch.cuda.Stream()
+        tlsgpu.seal_batch(obj, b, s)
+        s.synchronize()
+        del s
+    torch.cuda.synchronize()
+    free1 = torch.cuda.mem_get_info()[0]
+    # per-stream buffers kept for the process would hold 48 x 1 MiB here
+    assert free0 - free1 < 8 << 20, (free0, free1)
+    recs, _ = fullcheck.check_all(torch, oracle_mod, "aesgcm", np.frombuffer(key, np.uint8), inp,
+                                  np.arange(n) * L, np.full(n, L), out, np.arange(n) * (L + 16),
+                                  fullcheck.tls13_nonces(iv, 0, n),
+                                  np.frombuffer(bytes(tls13_aad(L)), np.uint8), np.zeros(n), np.full(n, 5))
+    assert recs == n

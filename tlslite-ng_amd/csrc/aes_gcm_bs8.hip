@@ -350,7 +350,14 @@ __device__ __forceinline__ void octet_job(const KC& kc, const tg_batch& b,
         // (profiles/r04/r4p/).
         if (!OPEN && mt && __all(!valid || nvl <= 8u * beta || (nvl == 8u * beta + 1u && blk0 == nc - 1u))) {
             uint4 ks[1] = {rkl};
-            if (valid && nvl == 8u * beta + 1u) ks[0] = xor4(gload16(reinterpret_cast<const uint8_t*>(mt + 2 * t + 1)), rkl);
+            if (valid && nvl == 8u * beta + 1u) {
+                // the lanes' rho mapping puts a lone last block on lane rho = 0,
+                // i.e. nc = 8 LPR beta + 1: the slot the mask kernels wrote
+#if defined(TG_DEBUG_ASSERT)
+                assert(lone_last_block<LPR>(nc));
+#endif
+                ks[0] = xor4(gload16(reinterpret_cast<const uint8_t*>(mt + 2 * t + 1)), rkl);
+            }
             consume(ks, blk0, 0, std::integral_constant<int, 1>(), nullptr);
         } else if (TROLE) {
             // through the 256-counter window cache when no lane of the wave
@@ -612,41 +619,10 @@ __global__ __launch_bounds__(1024) void hy_mask_kernel(const GcmKeyDev* __restri
         // full TLS 1.3 record's 16 385-byte inner plaintext -- gets that
         // block's keystream too (counter 2 + nc - 1, octet_job's tail path)
         const uint32_t nc = (rec_len(b, i) + 15) >> 4;
-        if (nc % 64u == 1u)
+        if (lone_last_block<8>(nc))
             gstore16(reinterpret_cast<uint8_t*>(masks + 2 * t + 1),
                      aes_block<NR>(lane4, rk, make_uint4(nv.x, nv.y, nv.z, bswap32(nc + 1u))));
     }
-}
-
-// The hybrid launch's scratch: job counter and batch copy (256 bytes), then
-// two 16-byte keystream blocks per record (hy_mask_kernel).  One buffer per (device,
-// stream) for the life of the process: launches on one stream are ordered,
-// so they can share it, and launches on different streams never do.  It grows
-// (at least doubling) when a batch needs more mask room; the outgrown buffer
-// is kept, not freed, because another host thread launching on the same
-// stream may already hold it (its launches stay stream-ordered with ours).
-// (Round 3 allocated scratch per launch with hipMallocAsync, and built the key
-// rows per launch in the setup kernel; both are gone from the per-call path.)
-// A stream handle reused after hipStreamDestroy inherits the buffer; the
-// destroyed stream's work has completed by then.
-uint8_t* hy_scratch(hipStream_t s, uint64_t nrec) {
-    struct Buf {
-        uint8_t* p;
-        uint64_t cap;   // records of mask room
-    };
-    static std::mutex mu;
-    static std::map<std::pair<int, hipStream_t>, Buf> pool;
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess) return nullptr;
-    std::lock_guard<std::mutex> g(mu);
-    auto it = pool.find({dev, s});
-    if (it != pool.end() && it->second.cap >= nrec) return it->second.p;
-    uint64_t cap = it != pool.end() ? it->second.cap : 0;
-    cap = nrec > 2 * cap ? nrec : 2 * cap;
-    uint8_t* p = nullptr;
-    if (hipMalloc((void**)&p, 256 + 32 * cap) != hipSuccess) return nullptr;
-    pool[{dev, s}] = Buf{p, cap};
-    return p;
 }
 
 template <int NR, bool OPEN>
@@ -656,6 +632,28 @@ int launch_bs8(const GcmKeyDev* key, const tg_batch& b, hipStream_t s, const uin
     if (groups > 0x7fffffffull) return TG_EINVAL;
     hipLaunchKernelGGL((gcm_bs8_kernel<NR, OPEN>), dim3((unsigned)groups), dim3(kBs8Threads), kBs8Lds, s,
                        key, b, order);
+    return hipGetLastError() == hipSuccess ? TG_OK : TG_EHIP;
+}
+
+// The mask and hybrid kernels of one launch_hy call, on its scratch.
+template <int NR, bool OPEN>
+int launch_hy_kernels(const GcmKeyDev* key, const tg_batch& b, hipStream_t s, const uint32_t* order, uint32_t nt,
+                      uint32_t prio, bool small, uint32_t* queue, tg_batch* bcopy, uint4* masks) {
+    if (masks && b.n) {
+        if (lds_attr((const void*)hy_mask_kernel<NR>, 65536)) return TG_EHIP;
+        const uint64_t wgs = (b.n + 1023) / 1024, cus = (uint64_t)device_cus();
+        const unsigned grid = (unsigned)(wgs < cus ? wgs : cus);   // persistent: at most one per CU
+        hipLaunchKernelGGL((hy_mask_kernel<NR>), dim3(grid), dim3(1024), 65536, s, key, b, order, masks);
+        if (hipGetLastError() != hipSuccess) return TG_EHIP;
+    }
+    const uint4* krows = reinterpret_cast<const uint4*>(key->bs8rows);
+    const uint4* rkrot = reinterpret_cast<const uint4*>(key->rkrot);
+    if (small)
+        hipLaunchKernelGGL((gcm_hy_kernel<NR, OPEN, 768>), dim3((unsigned)device_cus()), dim3(768), kHyLds, s,
+                           key, (const tg_batch*)bcopy, order, queue, nt, prio, krows, rkrot, masks);
+    else
+        hipLaunchKernelGGL((gcm_hy_kernel<NR, OPEN, 1024>), dim3((unsigned)device_cus()), dim3(1024), kHyLds,
+                           s, key, (const tg_batch*)bcopy, order, queue, nt, prio, krows, rkrot, masks);
     return hipGetLastError() == hipSuccess ? TG_OK : TG_EHIP;
 }
 
@@ -676,37 +674,31 @@ int launch_hy(const GcmKeyDev* key, const tg_batch& b, hipStream_t s, const uint
     const uint32_t prio = opt(kOptHyPrio) == 1 ? 1u : 0u;
     const void* fn = small ? (const void*)gcm_hy_kernel<NR, OPEN, 768> : (const void*)gcm_hy_kernel<NR, OPEN, 1024>;
     if (lds_attr(fn, (int)kHyLds)) return TG_EHIP;
-    // job counter + batch copy: per-stream scratch (hy_scratch); the key rows
-    // and rotated round keys come with the key (GcmKeyDev::bs8rows, rkrot)
+    // The launch's scratch -- job counter and batch copy (256 bytes), then two
+    // 16-byte keystream blocks per record (hy_mask_kernel) -- is allocated
+    // stream-ordered from the device's memory pool (stream_alloc: the pool
+    // keeps freed memory, so this is a host-side bookkeeping step, not a
+    // device allocation) and freed behind the kernel: nothing outlives the
+    // call, and launches on different streams (hipStreamPerThread included)
+    // never share it.  The key rows and rotated round keys come
+    // with the key (GcmKeyDev::bs8rows, rkrot).
 #if defined(TG_HY_NO_MASK)   // A/B builds: every wave computes its records' masks
-    uint8_t* scratch = hy_scratch(s, 0);
-    uint4* masks = nullptr;
+    const uint64_t mrec = 0;
 #else
-    uint8_t* scratch = hy_scratch(s, b.n);
-    uint4* masks = scratch ? reinterpret_cast<uint4*>(scratch + 256) : nullptr;
+    const uint64_t mrec = b.n;
 #endif
-    if (!scratch) return TG_EHIP;
+    uint8_t* scratch = nullptr;
+    if (stream_alloc((void**)&scratch, 256 + 32 * mrec, s)) return TG_EHIP;
+    uint4* masks = mrec ? reinterpret_cast<uint4*>(scratch + 256) : nullptr;
     uint32_t* queue = reinterpret_cast<uint32_t*>(scratch);
     tg_batch* bcopy = reinterpret_cast<tg_batch*>(scratch + 64);
     hipLaunchKernelGGL(hy_setup_kernel, dim3(1), dim3(64), 0, s, b, queue, bcopy);
-    if (hipGetLastError() != hipSuccess) return TG_EHIP;
-    if (masks && b.n) {
-        if (lds_attr((const void*)hy_mask_kernel<NR>, 65536)) return TG_EHIP;
-        const uint64_t wgs = (b.n + 1023) / 1024, cus = (uint64_t)device_cus();
-        const unsigned grid = (unsigned)(wgs < cus ? wgs : cus);   // persistent: at most one per CU
-        hipLaunchKernelGGL((hy_mask_kernel<NR>), dim3(grid), dim3(1024), 65536, s, key, b, order, masks);
-        if (hipGetLastError() != hipSuccess) return TG_EHIP;
-    }
-    const uint4* krows = reinterpret_cast<const uint4*>(key->bs8rows);
-    const uint4* rkrot = reinterpret_cast<const uint4*>(key->rkrot);
-    if (small)
-        hipLaunchKernelGGL((gcm_hy_kernel<NR, OPEN, 768>), dim3((unsigned)device_cus()), dim3(768), kHyLds, s,
-                           key, (const tg_batch*)bcopy, order, queue, nt, prio, krows, rkrot, masks);
-    else
-        hipLaunchKernelGGL((gcm_hy_kernel<NR, OPEN, 1024>), dim3((unsigned)device_cus()), dim3(1024), kHyLds,
-                           s, key, (const tg_batch*)bcopy, order, queue, nt, prio, krows, rkrot, masks);
-    return hipGetLastError() == hipSuccess ? TG_OK : TG_EHIP;
+    int rc = hipGetLastError() == hipSuccess ? TG_OK : TG_EHIP;
+    if (!rc) rc = launch_hy_kernels<NR, OPEN>(key, b, s, order, nt, prio, small, queue, bcopy, masks);
+    if (hipFreeAsync(scratch, s) != hipSuccess && !rc) rc = TG_EHIP;
+    return rc;
 }
+
 
 // ---- key tables: key-grouped octet jobs on bitsliced waves ----------------
 // A batch over a key table (config 4: many sessions, per-record key_idx) is
@@ -893,7 +885,7 @@ __global__ __launch_bounds__(1024) void kt_mask_kernel(const GcmTableKey* __rest
         // a record whose last batch row (8 x 32 blocks) holds one block: that
         // block's keystream, counter 2 + nc - 1 (octet_job's tail path)
         const uint32_t nc = (rec_len(b, i) + 15) >> 4;
-        if (nc % 256u == 1u)
+        if (lone_last_block<32>(nc))
             gstore16(reinterpret_cast<uint8_t*>(masks + 2 * t + 1),
                      aes_block<NR>(lane4, rk, make_uint4(nv.x, nv.y, nv.z, bswap32(nc + 1u))));
     }
@@ -1018,7 +1010,7 @@ int launch_kt(const GcmTableKey* keys, uint64_t nkeys, const uint4* hpow, const 
     const size_t sm = hybrid && lpr == 32 ? b.n * 32 + (b.n + 1) * 4 : 0;   // + kth_jobkey_kernel's keys
     const size_t po = (so + sj + 256 + plan + 255) & ~(size_t)255;
     uint8_t* buf = nullptr;
-    if (hipMallocAsync((void**)&buf, po + sm, s) != hipSuccess) return TG_EHIP;
+    if (stream_alloc((void**)&buf, po + sm, s)) return TG_EHIP;
     uint32_t* order = reinterpret_cast<uint32_t*>(buf);
     uint32_t* jobpos = reinterpret_cast<uint32_t*>(buf + so);
     uint32_t* njobs = reinterpret_cast<uint32_t*>(buf + so + sj);

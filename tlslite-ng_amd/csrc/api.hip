@@ -87,7 +87,7 @@ struct tg_key {
                             // AesKeyDev[nkeys] (AES-CCM), ChachaKeyDev[nkeys]
     std::mutex stage_mu;    // guards the two lists
     std::vector<Stage*> stages;        // every slot of this key
-    std::vector<Stage*> free_stages;   // the idle ones
+    std::vector<Stage*> free_stages;   // the idle ones (never trimmed before destroy)
 };
 
 namespace {
@@ -131,26 +131,14 @@ int take_stage(tg_key* k, Stage** out) {
     return TG_OK;
 }
 
-// Idle slots a key keeps; a slot given back beyond these is freed, so a burst
-// of concurrent calls does not pin its buffers for the key's lifetime.
-constexpr size_t kMaxIdleStages = 4;
-
+// A slot given back stays with the key until tg_key_destroy: the pool is as
+// large as the most calls the key has had in flight at once, so bursts of
+// concurrent calls reuse their slots instead of destroying streams and
+// freeing pinned memory (which can synchronise the device) after each burst
+// (ADVICE r04).
 void give_stage(tg_key* k, Stage* st) {
-    {
-        std::lock_guard<std::mutex> g(k->stage_mu);
-        if (k->free_stages.size() < kMaxIdleStages) {
-            k->free_stages.push_back(st);
-            return;
-        }
-        for (size_t i = 0; i < k->stages.size(); ++i)
-            if (k->stages[i] == st) {
-                k->stages[i] = k->stages.back();
-                k->stages.pop_back();
-                break;
-            }
-    }
-    (void)hipStreamSynchronize(st->stream);
-    free_stage(st);
+    std::lock_guard<std::mutex> g(k->stage_mu);
+    k->free_stages.push_back(st);
 }
 
 int ensure_stage(Stage* st, size_t bytes) {
@@ -291,7 +279,7 @@ int launch(tg_key* k, const tg_batch& b, bool open, hipStream_t s) {
     if (rc) return rc;
     const size_t obytes = (b.n * sizeof(uint32_t) + 255) & ~(size_t)255;
     uint8_t* buf = nullptr;
-    HIP_TRY(hipMallocAsync((void**)&buf, obytes + scratch, s));
+    if (tg::stream_alloc((void**)&buf, obytes + scratch, s)) return fail(TG_EHIP, "scratch allocation failed");
     uint32_t* order = reinterpret_cast<uint32_t*>(buf);
     rc = tg_length_order(b.len, b.n, order, buf + obytes, &scratch, s);
     if (!rc) rc = launch_kernels(k, b, open, s, order);
@@ -404,7 +392,7 @@ int records_scratch(uint64_t n, hipStream_t st, ScratchAlloc& a, tg::RecScratch&
     const size_t per = 8 + 8 + 4 + 12 + 16 + 4 + 1 + 1;
     const size_t bytes = per * n + 64 + 64;
     a.s = st;
-    HIP_TRY(hipMallocAsync(&a.base, bytes, st));
+    if (tg::stream_alloc(&a.base, bytes, st)) return fail(TG_EHIP, "scratch allocation failed");
     uint8_t* p = static_cast<uint8_t*>(a.base);
     s.in_abs = reinterpret_cast<uint64_t*>(p); p += 8 * n;
     s.out_abs = reinterpret_cast<uint64_t*>(p); p += 8 * n;
@@ -546,6 +534,24 @@ int lds_attr(const void* fn, int bytes) {
         return TG_EHIP;
     done.insert({fn, dev});
     return TG_OK;
+}
+
+int stream_alloc(void** p, size_t bytes, hipStream_t s) {
+    static std::mutex mu;
+    static std::set<int> pools;   // devices whose default pool keeps its memory
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return TG_EHIP;
+    {
+        std::lock_guard<std::mutex> g(mu);
+        if (!pools.count(dev)) {
+            hipMemPool_t pool = nullptr;
+            if (hipDeviceGetDefaultMemPool(&pool, dev) != hipSuccess) return TG_EHIP;
+            uint64_t keep = ~0ull;
+            if (hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &keep) != hipSuccess) return TG_EHIP;
+            pools.insert(dev);
+        }
+    }
+    return hipMallocAsync(p, bytes ? bytes : 1, s) == hipSuccess ? TG_OK : TG_EHIP;
 }
 
 // tg_version()'s text; a measurement build appends its flags (common.h).

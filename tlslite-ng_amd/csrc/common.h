@@ -268,9 +268,29 @@ struct RecScratch {
     uint8_t* dummy;       // 32 zero bytes: AEAD input of publicly-invalid records
 };
 
+// The per-slot keystream precompute of the AES-GCM octet / pair jobs
+// (aes_gcm_bs8.hip): a record of nc blocks whose last batch row (8 blocks of
+// each of its LPR lanes) holds only its last block -- nc % (8 LPR) == 1, e.g.
+// a full TLS 1.3 record's 16 385-byte inner plaintext -- gets that block's
+// keystream at mask slot 2 t + 1 (hy_mask_kernel: LPR 8, kt_mask_kernel: LPR
+// 32), and octet_job's seal path reads it exactly then.  One definition for
+// the writers and the reader.
+template <int LPR>
+__host__ __device__ constexpr bool lone_last_block(uint32_t nc) {
+    return nc % (8u * LPR) == 1u;
+}
+
 // hipFuncSetAttribute(MaxDynamicSharedMemorySize) for ``fn`` on the current
 // device, once per (function, device); thread-safe (api.hip).  0 or TG_EHIP.
 int lds_attr(const void* fn, int bytes);
+
+// Stream-ordered scratch (hipMallocAsync on ``s``) from the current device's
+// default memory pool, whose release threshold is raised to "keep
+// everything" on first use per device: a freed block (hipFreeAsync) stays in
+// the pool for the next launch, so per-launch scratch costs host bookkeeping
+// and no device allocation, and nothing outlives its launch (api.hip).
+// 0 or TG_EHIP.
+int stream_alloc(void** p, size_t bytes, hipStream_t s);
 
 // Compute units of the current device (grid size of the persistent kernels),
 // looked up once per device.

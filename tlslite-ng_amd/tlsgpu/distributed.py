@@ -43,8 +43,9 @@ def init_process(torch, dist, backend=None, use_gpu=True, group_at_world1=None):
     A process group is created for world > 1, and also at world 1 when
     ``group_at_world1`` (default: TLSGPU_DIST_SELFTEST=1) asks for it, so the
     collectives below run through the backend on a one-GPU box too (the RCCL
-    self-test, bench.py --dist-selftest).  Outside torch.distributed.run the
-    rendezvous is tcp://127.0.0.1 on a free port.
+    self-test, bench.py --dist-selftest).  Without MASTER_ADDR the world-1
+    group rendezvouses on tcp://127.0.0.1 at a free port; at world > 1 every
+    rank would pick a different port and hang, so that is a DistError.
     Returns (world, rank, local_rank, device or None)."""
     world, rank, local = env_rank()
     backend = backend or os.environ.get("TLSGPU_DIST_BACKEND", "nccl")
@@ -65,6 +66,9 @@ def init_process(torch, dist, backend=None, use_gpu=True, group_at_world1=None):
     if world > 1 or group_at_world1:
         kw = {}
         if "MASTER_ADDR" not in os.environ:
+            if world > 1:
+                raise DistError("WORLD_SIZE=%d without MASTER_ADDR: launch the ranks with "
+                                "torch.distributed.run (--master-addr 127.0.0.1)" % world)
             kw = {"init_method": "tcp://127.0.0.1:%d" % _free_port(), "world_size": world,
                   "rank": rank}
         if backend == "nccl":
@@ -171,6 +175,22 @@ def reduce_counters(torch, dist, counters, elapsed, device=None):
         dist.all_reduce(c, op=dist.ReduceOp.SUM)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return [float(x) for x in c.tolist()], float(t.item())
+
+
+def reduce_verification(torch, dist, ok, mismatches, checked, device=None):
+    """The N > 1 line's verification over all ranks: ``ok`` is the MIN of the
+    ranks' flags (one failing shard fails the line), ``mismatches`` and
+    ``checked`` (oracle-compared records) the SUMs.  Returns
+    (ok, mismatches, checked)."""
+    if group_active(dist) and dist.get_backend() == "gloo":
+        device = None   # gloo's MIN over CPU tensors (the rehearsal backend)
+    t = torch.tensor([1.0 if ok else 0.0], dtype=torch.float64, device=device)
+    c = torch.tensor([float(mismatches), float(checked)], dtype=torch.float64, device=device)
+    if group_active(dist):
+        dist.all_reduce(t, op=dist.ReduceOp.MIN)
+        dist.all_reduce(c, op=dist.ReduceOp.SUM)
+    m, n = c.tolist()
+    return bool(t.item() == 1.0), int(m), int(n)
 
 
 def gather_rows(torch, dist, row, device=None):

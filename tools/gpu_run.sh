@@ -1,0 +1,66 @@
+#!/bin/bash
+# One GPU call, any mix of steps, each under its own time limit; the first
+# failing step ends the script (set -e).  Output under gpurun_out/<tag>/.
+#   bash tools/gpu_run.sh <tag> step [step ...]
+# steps:
+#   tests[=EXPR]   pytest -m gpu (-k EXPR)            -> pytest.log
+#   smoke          __graft_entry__.smoke()             -> smoke.log
+#   bench          bench.py (headline, CPU baseline)   -> bench.json
+#   bench-nocpu    bench.py --no-cpu-baseline          -> bench.json
+#   c4 | c5 | ccm | c1 | e2e | ingest                  -> bench_<step>.json
+#   n2             bench.py --gpus 2 --config c5 --records 65536 over gloo on
+#                  one MI355X (both ranks on the one device), CPU baseline on
+#                  -> bench_n2_c5.json; and the headline leg -> bench_n2.json
+#   prof           rocprofv3 --kernel-trace --stats of bench.py --no-cpu-baseline
+#                  -> kernel_stats.csv
+#   pmc            tools/pmc_full.sh passes of the headline kernels
+#   traffic        tools/traffic.sh FETCH_SIZE / WRITE_SIZE passes -> traffic.json
+#   ab=LIBA,LIBB   alternate two built libraries (tools/gpu_lib_ab.sh) -> ab.txt
+# Environment passes through (TLSGPU_* options, BENCH_ARGS for bench steps).
+set -e
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+T=$1; shift
+O=$R/gpurun_out/$T; mkdir -p $O
+cd $R
+for st in "$@"; do
+  echo "== $st $(date +%T)"
+  case $st in
+    tests|tests=*)
+      K=${st#tests}; K=${K#=}
+      if [ -n "$K" ]; then
+        timeout -k 10 1100 python -u -m pytest tests -m gpu -x -q --timeout 400 --timeout-method thread -k "$K" > $O/pytest.log 2>&1 || { tail -40 $O/pytest.log; exit 1; }
+      else
+        timeout -k 10 1100 python -u -m pytest tests -m gpu -x -q --timeout 400 --timeout-method thread > $O/pytest.log 2>&1 || { tail -40 $O/pytest.log; exit 1; }
+      fi
+      tail -3 $O/pytest.log ;;
+    smoke)
+      timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1
+      tail -1 $O/smoke.log ;;
+    bench)
+      timeout -k 10 600 python -u bench.py $BENCH_ARGS > $O/bench.json 2> $O/bench.err; cat $O/bench.json ;;
+    bench-nocpu)
+      timeout -k 10 600 python -u bench.py --no-cpu-baseline $BENCH_ARGS > $O/bench.json 2> $O/bench.err; cat $O/bench.json ;;
+    c4|c5|ccm|c1|ingest)
+      timeout -k 10 600 python -u bench.py --config $st $BENCH_ARGS > $O/bench_$st.json 2> $O/bench_$st.err; cat $O/bench_$st.json ;;
+    e2e)
+      timeout -k 10 600 python -u bench.py --e2e --no-cpu-baseline $BENCH_ARGS > $O/bench_e2e.json 2> $O/bench_e2e.err; cat $O/bench_e2e.json ;;
+    n2)
+      TLSGPU_DIST_BACKEND=gloo timeout -k 10 400 python -u bench.py --gpus 2 --config c5 --records 65536 \
+        --steps 3 --warmup 1 > $O/bench_n2_c5.json 2> $O/bench_n2_c5.err; cat $O/bench_n2_c5.json
+      TLSGPU_DIST_BACKEND=gloo timeout -k 10 400 python -u bench.py --gpus 2 --records 65536 \
+        --steps 3 --warmup 1 > $O/bench_n2.json 2> $O/bench_n2.err; cat $O/bench_n2.json ;;
+    prof)
+      (cd /tmp && export TMPDIR=/tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv \
+        -d $O/prof -o run -- python3 $R/bench.py --no-cpu-baseline $BENCH_ARGS > $O/prof.log 2>&1)
+      find $O/prof -name "*kernel_stats.csv" -exec cp {} $O/kernel_stats.csv \;
+      head -12 $O/kernel_stats.csv ;;
+    pmc)
+      bash tools/pmc_full.sh $T ;;
+    traffic)
+      bash tools/traffic.sh $T ;;
+    ab=*)
+      L=${st#ab=}; bash tools/gpu_lib_ab.sh $T ${L%,*} ${L#*,} ;;
+    *) echo "unknown step $st"; exit 2 ;;
+  esac
+done
+echo "== done $(date +%T)"
