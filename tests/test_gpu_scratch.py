@@ -28,19 +28,26 @@ def test_many_streams_memory_flat(oracle_mod):
     aad = torch.tensor(list(tls13_aad(L)), dtype=torch.uint8, device="cuda")
     b = tlsgpu.make_batch(n, inp, out, nonces, aad=aad, fixed_len=L, in_stride=L, out_stride=L + 16,
                           fixed_aad_len=5)
-    s0 = torch.cuda.Stream()
-    tlsgpu.seal_batch(obj, b, s0)          # first use: the pool grows once
+    # torch hands out its pool of 32 streams round robin: 40 streams use all
+    # of them.  Each stream first runs a ChaCha20-Poly1305 batch (no
+    # per-launch scratch), so whatever the runtime keeps per stream is there
+    # before the count starts; then one AES-GCM batch per stream.
+    chacha = tlsgpu.HipCHACHA20_POLY1305(bytearray(32))
+    streams = [torch.cuda.Stream() for _ in range(40)]
+    tlsgpu.seal_batch(obj, b)                 # the pool's first block
+    for st in streams:
+        tlsgpu.seal_batch(chacha, b, st)
     torch.cuda.synchronize()
     free0 = torch.cuda.mem_get_info()[0]
-    for k in range(48):                    # a new stream per batch, dropped after it
-        s = torch.cuda.Stream()
-        tlsgpu.seal_batch(obj, b, s)
-        s.synchronize()
-        del s
+    for st in streams:
+        tlsgpu.seal_batch(obj, b, st)
+        st.synchronize()
     torch.cuda.synchronize()
     free1 = torch.cuda.mem_get_info()[0]
-    # per-stream buffers kept for the process would hold 48 x 1 MiB here
+    # per-stream buffers kept for the process would hold 32 x 1 MiB here
     assert free0 - free1 < 8 << 20, (free0, free1)
+    tlsgpu.seal_batch(obj, b)
+    torch.cuda.synchronize()
     recs, _ = fullcheck.check_all(torch, oracle_mod, "aesgcm", np.frombuffer(key, np.uint8), inp,
                                   np.arange(n) * L, np.full(n, L), out, np.arange(n) * (L + 16),
                                   fullcheck.tls13_nonces(iv, 0, n),

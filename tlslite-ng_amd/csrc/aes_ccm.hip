@@ -27,6 +27,7 @@
 // 128-bit increment would carry into the nonce (tlsgpu.h documents the limit).
 #include <stdlib.h>
 
+#include "aes_bs8.h"
 #include "aes_round.h"
 #include "options.h"
 
@@ -385,6 +386,259 @@ __global__ __launch_bounds__(kCcmWaveThreads) void ccm_wave_kernel(const AesKeyD
     }
 }
 
+// ---- hybrid lane-per-record kernel (large single-key batches) ----------
+// The lane kernel above runs both AES streams of a block as T-table rounds
+// (~293 LDS lookups per block) and is bound by the LDS.  Here the keystream
+// of most records comes from the 8-block bitsliced cipher (aes_bs8.h) on the
+// VALU, and only the serial CBC-MAC chain stays on the T-table rounds:
+//   * a lane owns a record (as in ccm_kernel); batch beta of the lane is its
+//     blocks 8 beta .. 8 beta + 7, i.e. counters S_(8 beta + 1 .. 8 beta + 8)
+//     -- eight consecutive counters, the bs8 counter layout with SB = 0
+//     (blocks one apart): counter bits 0..2 per block, bits >= 3 from beta,
+//     the same for every lane of the wave (aesccm.py:36-38, :72-83);
+//   * the counter block flags || nonce || be24(j) has bytes 0..12 constant
+//     per record (nonce[11] is row 0 of column 3, where GCM has a zero
+//     counter byte) and bytes 14..15 in rows 2-3 of column 3 exactly where
+//     the GCM counter's low bytes sit, so round 1's S-box of rows 0-1 is a
+//     per-record constant (kept in a lane-private LDS area) while the
+//     counter stays below 2^16;
+//   * the eight keystream blocks of a batch go to the payload (CTR) and the
+//     eight plaintext blocks through the MAC chain x = E(x ^ m) by T-table
+//     rounds (aes_block), the batch's payload loaded ahead of the chain.
+// Waves 0 .. nt - 1 run the whole record on T-table rounds (ccm_record,
+// the lane kernel's code), the rest as above; all take 64-record jobs from
+// one queue, so the LDS pipe (MAC chains, T-table keystreams) and the VALU
+// (bitsliced keystreams) are busy at the same time -- the AES-GCM hybrid's
+// split (aes_gcm_bs8.hip gcm_hy_kernel).
+constexpr int kCcmHyThreads = 768;                        // 12 waves (3 per SIMD, <= 168 VGPRs)
+constexpr uint32_t kCcmHyRows = 65536;                    // after the Te block
+constexpr uint32_t kCcmHyRowArea = 16 * 64 * 4;           // rows 0-1 planes, lane-major
+constexpr uint32_t kCcmHyRk = kCcmHyRows + (kCcmHyThreads / 64) * kCcmHyRowArea;   // round keys
+constexpr size_t kCcmHyLds = kCcmHyRk + 240;
+constexpr int kCcmHyTDefault = 4;
+
+// aes_block with the middle rounds as a loop: the MAC steps of a bitsliced
+// batch are eight dependent blocks, and unrolled they spilled the cipher's
+// registers.
+template <int NR, class RK>
+__device__ __forceinline__ uint4 aes_block_rolled(uint32_t lane4, const RK& rkp, uint4 in) {
+    const uint4 k0 = rkp.get(0);
+    uint32_t s0 = in.x ^ k0.x, s1 = in.y ^ k0.y, s2 = in.z ^ k0.z, s3 = in.w ^ k0.w;
+#pragma unroll 1
+    for (int r = 1; r < NR; ++r) {
+        const uint4 k = rkp.get(r);
+        const uint32_t t0 = col(s0, s1, s2, s3, k.x, lane4);
+        const uint32_t t1 = col(s1, s2, s3, s0, k.y, lane4);
+        const uint32_t t2 = col(s2, s3, s0, s1, k.z, lane4);
+        const uint32_t t3 = col(s3, s0, s1, s2, k.w, lane4);
+        s0 = t0; s1 = t1; s2 = t2; s3 = t3;
+    }
+    const uint4 k = rkp.get(NR);
+    return make_uint4(col_last(s0, s1, s2, s3, k.x, lane4), col_last(s1, s2, s3, s0, k.y, lane4),
+                      col_last(s2, s3, s0, s1, k.z, lane4), col_last(s3, s0, s1, s2, k.w, lane4));
+}
+
+template <int NR, bool OPEN, int TAG>
+__device__ __forceinline__ void ccm_bs_record(const tg_batch& b, uint64_t i, bool valid, uint32_t lane4,
+                                              const RkLds& rk, const bs8::KeyPlanesVmemFolded& km,
+                                              uint32_t rows) {
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint8_t* in = valid ? rec_in(b, i) : nullptr;
+    uint8_t* out = valid ? rec_out(b, i) : nullptr;
+    const uint32_t len = valid ? rec_len(b, i) : 0u;
+    const uint8_t* ad = valid ? rec_aad(b, i) : nullptr;
+    const uint32_t alen = valid ? rec_aad_len(b, i) : 0u;
+    const bool aligned = (((uintptr_t)in | (uintptr_t)out) & 15) == 0;
+    const uint4 nv = valid ? load_partial(b.nonce + 12 * i, 12) : make_uint4(0, 0, 0, 0);
+    const uint32_t a0 = 2u | (nv.x << 8);
+    const uint32_t a1 = (nv.x >> 24) | (nv.y << 8);
+    const uint32_t a2 = (nv.y >> 24) | (nv.z << 8);
+    const uint32_t a3 = nv.z >> 24;                       // n11, counter bytes zero
+    // the first state's per-record words (S_j ^ rk0 without the counter)
+    const uint4 k0 = rk.get(0);
+    const uint32_t u[4] = {a0 ^ k0.x, a1 ^ k0.y, a2 ^ k0.z, a3 ^ k0.w};
+    // rows 0 and 1 after round 1's SubBytes: no counter byte below 2^16
+    {
+        uint32_t r0[8], r1[8];
+#pragma unroll
+        for (int bb = 0; bb < 8; ++bb) {
+            r0[bb] = bs8::rec_plane(u, bb);
+            r1[bb] = bs8::rec_plane(u, 8 + bb);
+        }
+        bs::sbox(r0);
+        bs::sbox(r1);
+#pragma unroll
+        for (int bb = 0; bb < 8; ++bb) {
+            lds_st32(rows + 4u * (64u * bb + lane), r0[bb]);
+            lds_st32(rows + 4u * (64u * (8 + bb) + lane), r1[bb]);
+        }
+    }
+    // the last round key (the bitsliced rounds leave it out; its planes
+    // carry the S-box constant, see aes_bs8.h)
+    const uint4 kl = rk.get(NR);
+    const uint4 rkl = make_uint4(kl.x ^ 0x63636363u, kl.y ^ 0x63636363u, kl.z ^ 0x63636363u, kl.w ^ 0x63636363u);
+    uint32_t lanec[3], kmask;
+    bs8::lane_consts<0>(1u, lanec, kmask);                // block j of a batch: counter 8 beta + 1 + j
+
+    // E(S_0) masks the tag; B_0 and the AAD blocks start the MAC (aesccm.py:40-67)
+    const uint4 s0 = aes_block<NR>(lane4, rk, make_uint4(a0, a1, a2, a3));
+    uint4 x = make_uint4(0, 0, 0, 0);
+    if (valid)
+        ccm_mac_head<TAG>([&](uint4 blk) { x = aes_block<NR>(lane4, rk, xor_blk(x, blk)); }, nv, a1, a2, a3,
+                          len, ad, alen);
+    const uint32_t nfull = len >> 4, tail = len & 15, nblk = (len + 15) >> 4;
+    uint32_t nb = (nblk + 7) >> 3;
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) {
+        const uint32_t o = (uint32_t)__shfl_xor((int)nb, off, 64);
+        nb = o > nb ? o : nb;
+    }
+    nb = (uint32_t)__builtin_amdgcn_readfirstlane((int)nb);
+    uint32_t u0 = u[0], u1 = u[1], u2 = u[2], u3 = u[3];
+    for (uint32_t beta = 0; beta < nb; ++beta) {
+        const uint32_t blk0 = 8u * beta;
+        // the planes are rebuilt (rows 2-3) and re-read (rows 0-1) per batch:
+        // hoisted out of the loop they held 32 more registers across the
+        // cipher and spilled
+        asm volatile("" : "+v"(u0), "+v"(u1), "+v"(u2), "+v"(u3) :: "memory");
+        const uint32_t uu[4] = {u0, u1, u2, u3};
+        const bool hi = (beta + 1u) >> 13;                // counters >= 2^16 (records over 1 MiB)
+        uint32_t s[4][8];
+#pragma unroll
+        for (int bb = 0; bb < 8; ++bb) {
+            s[0][bb] = hi ? bs8::rec_plane(uu, bb) : lds_u32(rows + 4u * (64u * bb + lane));
+            s[1][bb] = hi ? bs8::rec_plane(uu, 8 + bb) : lds_u32(rows + 4u * (64u * (8 + bb) + lane));
+            s[2][bb] = bs8::rec_plane(uu, 16 + bb);
+            s[3][bb] = bs8::rec_plane(uu, 24 + bb);
+        }
+#pragma unroll
+        for (int bb = 0; bb < 3; ++bb) s[3][bb] ^= lanec[bb];
+        bs8::ctr_planes<3, 16, 3>(s, kmask, beta);
+        if (hi) bs8::ctr_planes<16, 32, 3>(s, kmask, beta);
+        uint32_t w[4][8];
+        bs8::encrypt<NR>(s, km, w, hi);
+        __builtin_amdgcn_sched_barrier(0);   // the payload loads stay behind the cipher
+        if (!valid) continue;
+        // the batch's payload (held across the cipher it would spill): the
+        // eight loads go out together, the MAC chain waits for the first
+        uint4 d[8];
+        const bool full = blk0 + 8u <= nfull;
+        if (full) {
+#pragma unroll
+            for (int j = 0; j < 8; ++j) d[j] = load16(in + 16u * (blk0 + j), aligned);
+        }
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const uint4 ks = make_uint4(w[0][j] ^ rkl.x, w[1][j] ^ rkl.y, w[2][j] ^ rkl.z, w[3][j] ^ rkl.w);
+            const uint32_t blk = blk0 + j;
+            uint4 m = make_uint4(0, 0, 0, 0);
+            if (full || blk < nfull) {
+                const uint4 dd = full ? d[j] : load16(in + 16u * blk, aligned);
+                const uint4 c = xor4(dd, ks);
+                store16(out + 16u * blk, c, aligned);
+                m = OPEN ? c : dd;
+            } else if (blk < nblk) {                      // the partial last block
+                const uint4 dd = load_partial(in + 16u * blk, tail);
+                const uint4 c = mask_tail(xor4(dd, ks), tail);
+                store_partial(out + 16u * blk, c, tail);
+                m = OPEN ? c : dd;
+            }
+            if (blk < nblk) x = aes_block_rolled<NR>(lane4, rk, xor_blk(x, m));
+        }
+    }
+    if (!valid) return;
+    const uint4 t = xor4(x, s0);   // the auth value; CCM_8 keeps its first 8 bytes
+    if (!OPEN) {
+        if (TAG == 16) {
+            store16(out + len, t, aligned && tail == 0);
+        } else {
+            store_partial(out + len, t, 8);
+        }
+        return;
+    }
+    // open: received_mac != computed_mac -> None (aesccm.py:144-146)
+    const uint4 exp = TAG == 16 ? load16(in + len, aligned && tail == 0) : load_partial(in + len, 8);
+    uint32_t diff = (exp.x ^ t.x) | (exp.y ^ t.y);
+    if (TAG == 16) diff |= (exp.z ^ t.z) | (exp.w ^ t.w);
+    if (b.status) b.status[i] = diff == 0;
+    if (diff) {
+        const uint4 z = make_uint4(0, 0, 0, 0);
+        for (uint32_t k = 0; k < nfull; ++k) store16(out + 16 * k, z, aligned);
+        if (tail) store_partial(out + 16 * nfull, z, tail);
+    }
+}
+
+template <int NR, bool OPEN, int TAG>
+__global__ __launch_bounds__(kCcmHyThreads) void ccm_hy_kernel(const AesKeyDev* __restrict__ key,
+                                                               const tg_batch* bp,
+                                                               const uint4* __restrict__ krows,
+                                                               uint32_t* __restrict__ queue, uint32_t nt) {
+    stage_te(reinterpret_cast<uint32_t*>(g_lds_ccm));   // Te0/Te2 copies at LDS 0
+    // the round keys from LDS (broadcast reads): the bitsliced role's key rows
+    // arrive by scalar loads, and both in SGPRs spilled
+    if (threadIdx.x < 4 * (NR + 1))
+        reinterpret_cast<uint32_t*>(g_lds_ccm)[kCcmHyRk / 4 + threadIdx.x] = key->rk[threadIdx.x];
+    const RkLds rk{kCcmHyRk};
+    __syncthreads();
+    const uint32_t wave = (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    const uint32_t lane4 = (threadIdx.x & 31u) << 2;
+    const uint64_t njobs = (bp->n + 63) / 64;
+    const uint32_t rows = kCcmHyRows + wave * kCcmHyRowArea;
+    for (;;) {
+        uint32_t job = 0;
+        if ((threadIdx.x & 63u) == 0) job = atomicAdd(queue, 1u);
+        job = (uint32_t)__builtin_amdgcn_readfirstlane((int)job);
+        if (job >= njobs) break;
+        // the batch descriptor re-read per job (device copy): held in SGPRs
+        // across the persistent loop it crowds out the ciphers' own scalars
+        asm volatile("" ::: "memory");
+        const tg_batch b = *bp;
+        const uint64_t i = 64ull * job + (threadIdx.x & 63u);
+        const bool valid = i < b.n;
+        if (wave < nt) {
+            if (valid) ccm_record<NR, OPEN, TAG, true>(b, i, lane4, rk);
+        } else {
+            ccm_bs_record<NR, OPEN, TAG>(b, i, valid, lane4, rk, bs8::KeyPlanesVmemFolded{{krows}}, rows);
+        }
+    }
+}
+
+// The hybrid kernel's scratch: the job counter, a device copy of the batch
+// descriptor at word 16, then the key's bitsliced rows at word 128
+// (aes_bs8.h KeyPlanesVmem layout, keymath.h bs8_row_word: the
+// MixColumns-folded planes of the middle rounds), 480 words.
+constexpr size_t kCcmHyScratch = 512 + 15 * 32 * 4;
+static_assert(sizeof(tg_batch) <= 512 - 64, "batch copy");
+__global__ void ccm_hy_setup_kernel(const AesKeyDev* __restrict__ key, int nr, tg_batch b, uint32_t* scratch) {
+    const int t = (int)threadIdx.x;
+    if (t == 0) {
+        scratch[0] = 0;
+        *reinterpret_cast<tg_batch*>(scratch + 16) = b;
+    }
+    for (int w = t; w < 15 * 32; w += (int)blockDim.x) scratch[128 + w] = bs8_row_word(key->rk, nr, w);
+}
+
+template <int NR, bool OPEN, int TAG>
+int launch_hy(const AesKeyDev* key, const tg_batch& b, hipStream_t s) {
+    const int o = opt(kOptCcmHyT);
+    if (o > kCcmHyThreads / 64) return TG_EINVAL;
+    const uint32_t nt = o < 0 ? 0u : o == 0 ? (uint32_t)kCcmHyTDefault : (uint32_t)o;
+    if (lds_attr((const void*)ccm_hy_kernel<NR, OPEN, TAG>, (int)kCcmHyLds)) return TG_EHIP;
+    if ((b.n + 63) / 64 > 0xffffffffull) return TG_EINVAL;
+    uint32_t* scratch = nullptr;
+    if (stream_alloc((void**)&scratch, kCcmHyScratch, s)) return TG_EHIP;
+    hipLaunchKernelGGL(ccm_hy_setup_kernel, dim3(1), dim3(256), 0, s, key, NR, b, scratch);
+    int rc = hipGetLastError() == hipSuccess ? TG_OK : TG_EHIP;
+    if (!rc) {
+        hipLaunchKernelGGL((ccm_hy_kernel<NR, OPEN, TAG>), dim3((unsigned)device_cus()), dim3(kCcmHyThreads),
+                           kCcmHyLds, s, key, reinterpret_cast<const tg_batch*>(scratch + 16),
+                           reinterpret_cast<const uint4*>(scratch + 128), scratch, nt);
+        rc = hipGetLastError() == hipSuccess ? TG_OK : TG_EHIP;
+    }
+    if (hipFreeAsync(scratch, s) != hipSuccess && !rc) rc = TG_EHIP;
+    return rc;
+}
+
 template <int NR, bool OPEN, int TAG, bool TABLE>
 int launch_wave(const AesKeyDev* keys, uint64_t nkeys, const tg_batch& b, hipStream_t s) {
     if (lds_attr((const void*)ccm_wave_kernel<NR, OPEN, TAG, TABLE>, (int)kCcmWaveLds)) return TG_EHIP;
@@ -413,7 +667,7 @@ int launch_w(const AesKeyDev* keys, uint64_t nkeys, const tg_batch& b, hipStream
 // Option ccm_variant (tests and measurement): 0 = auto (wave per record up
 // to kCcmWaveMaxRecords, else lane per record with the window cache), 1 =
 // lane per record, full rounds, 2 = wave per record, 3 = lane per record
-// with the window cache.
+// with the window cache, 4 = the hybrid lane-per-record kernel (single key).
 template <int NR, bool OPEN, int TAG, bool TABLE>
 int launch(const AesKeyDev* keys, uint64_t nkeys, const tg_batch& b, hipStream_t s) {
     switch (opt(kOptCcmVariant)) {
@@ -423,6 +677,9 @@ int launch(const AesKeyDev* keys, uint64_t nkeys, const tg_batch& b, hipStream_t
         case 1: return launch_w<NR, OPEN, TAG, TABLE, false>(keys, nkeys, b, s);
         case 2: return launch_wave<NR, OPEN, TAG, TABLE>(keys, nkeys, b, s);
         case 3: return launch_w<NR, OPEN, TAG, TABLE, true>(keys, nkeys, b, s);
+        case 4:
+            if (TABLE) return launch_w<NR, OPEN, TAG, TABLE, true>(keys, nkeys, b, s);
+            return launch_hy<NR, OPEN, TAG>(keys, b, s);
         default: return TG_EINVAL;
     }
 }

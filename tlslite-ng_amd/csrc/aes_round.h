@@ -63,6 +63,9 @@ __device__ __forceinline__ uint4 lds_u128(uint32_t addr) { return *(lds_u128_ptr
 __device__ __forceinline__ void lds_st128(uint32_t addr, uint4 v) {
     *(__attribute__((address_space(3))) uint4*)(uintptr_t)addr = v;
 }
+__device__ __forceinline__ void lds_st32(uint32_t addr, uint32_t v) {
+    *(__attribute__((address_space(3))) uint32_t*)(uintptr_t)addr = v;
+}
 __device__ __forceinline__ uint4 lds_u128_v(uint32_t addr) {
     const volatile __attribute__((address_space(3))) uint4* p =
         (const volatile __attribute__((address_space(3))) uint4*)(uintptr_t)addr;
@@ -81,6 +84,7 @@ __device__ __forceinline__ uint32_t lds_u32(uint32_t) { return 0; }
 __device__ __forceinline__ uint4 lds_u128(uint32_t) { return uint4(); }
 __device__ __forceinline__ uint4 lds_u128_v(uint32_t) { return uint4(); }
 __device__ __forceinline__ void lds_st128(uint32_t, uint4) {}
+__device__ __forceinline__ void lds_st32(uint32_t, uint32_t) {}
 __device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) { return a ^ b ^ c; }
 __device__ __forceinline__ uint32_t and_or(uint32_t a, uint32_t b, uint32_t c) { return (a & b) | c; }
 #endif

@@ -29,6 +29,7 @@ constexpr OptName kNames[kOptCount] = {
     {"hy_threads", "TLSGPU_HY_THREADS"},
     {"kt_hybrid", "TLSGPU_KT_HYBRID"},
     {"kt_t", "TLSGPU_KT_T"},
+    {"ccm_hy_t", "TLSGPU_CCM_HY_T"},
 };
 
 std::atomic<int> g_val[kOptCount];

@@ -16,14 +16,20 @@
 #   pmc            tools/pmc_full.sh passes of the headline kernels
 #   traffic        tools/traffic.sh FETCH_SIZE / WRITE_SIZE passes -> traffic.json
 #   ab=LIBA,LIBB   alternate two built libraries (tools/gpu_lib_ab.sh) -> ab.txt
-# Environment passes through (TLSGPU_* options, BENCH_ARGS for bench steps).
+# A step may carry its own environment after '@' (comma-separated, e.g.
+# ccm@TLSGPU_CCM_VARIANT=4,TLSGPU_CCM_HY_T=-1); its output file then takes the
+# suffix after '@' with '=' and ',' replaced.  Environment passes through
+# (TLSGPU_* options, BENCH_ARGS for bench steps).
 set -e
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 T=$1; shift
 O=$R/gpurun_out/$T; mkdir -p $O
 cd $R
-for st in "$@"; do
-  echo "== $st $(date +%T)"
+for st0 in "$@"; do
+  echo "== $st0 $(date +%T)"
+  st=${st0%%@*}; SUF=""; ENVS=""
+  if [ "$st" != "$st0" ]; then ENVS=${st0#*@}; SUF=_$(echo "$ENVS" | tr '=,' '-_'); fi
+  for kv in ${ENVS//,/ }; do export "$kv"; done
   case $st in
     tests|tests=*)
       K=${st#tests}; K=${K#=}
@@ -41,7 +47,8 @@ for st in "$@"; do
     bench-nocpu)
       timeout -k 10 600 python -u bench.py --no-cpu-baseline $BENCH_ARGS > $O/bench.json 2> $O/bench.err; cat $O/bench.json ;;
     c4|c5|ccm|c1|ingest)
-      timeout -k 10 600 python -u bench.py --config $st $BENCH_ARGS > $O/bench_$st.json 2> $O/bench_$st.err; cat $O/bench_$st.json ;;
+      timeout -k 10 600 python -u bench.py --config $st $BENCH_ARGS > $O/bench_$st$SUF.json 2> $O/bench_$st$SUF.err
+      cat $O/bench_$st$SUF.json ;;
     e2e)
       timeout -k 10 600 python -u bench.py --e2e --no-cpu-baseline $BENCH_ARGS > $O/bench_e2e.json 2> $O/bench_e2e.err; cat $O/bench_e2e.json ;;
     n2)
@@ -62,5 +69,6 @@ for st in "$@"; do
       L=${st#ab=}; bash tools/gpu_lib_ab.sh $T ${L%,*} ${L#*,} ;;
     *) echo "unknown step $st"; exit 2 ;;
   esac
+  for kv in ${ENVS//,/ }; do unset "${kv%%=*}"; done
 done
 echo "== done $(date +%T)"

@@ -4,7 +4,7 @@
 
 PROF_RECORDS / PROF_LEN: batch shape (2^18 x 16 KiB); sealed records at
 bench.py's 128-byte aligned stride; PROF_REPS: seal + open rounds (1);
-PROF_ALGS: which AEADs; PROF_OPTS: tlsgpu options as name=value,... (e.g.
+PROF_ALGS: which AEADs (aes128gcm, chacha20-poly1305, aes128ccm); PROF_OPTS: tlsgpu options as name=value,... (e.g.
 hy_t=16 for a hybrid kernel of T-table waves only, hy_t=-1 for bitsliced
 waves only).
 """
@@ -37,8 +37,9 @@ def main():
     tlsgpu.make_nonces(bytes(12), 0, n, nonces)
     aad = torch.tensor(list(tls13_aad(L)), dtype=torch.uint8, device="cuda")
     for a in algs:
-        c = tlsgpu.HipAESGCM(bytearray(16)) if a == "aes128gcm" else \
-            tlsgpu.HipCHACHA20_POLY1305(bytearray(32))
+        c = (tlsgpu.HipAESGCM(bytearray(16)) if a == "aes128gcm" else
+             tlsgpu.HipAESCCM(bytearray(16)) if a == "aes128ccm" else
+             tlsgpu.HipCHACHA20_POLY1305(bytearray(32)))
         for _ in range(reps):
             tlsgpu.seal_batch(c, tlsgpu.make_batch(n, inp, sealed, nonces, aad=aad, fixed_len=L,
                                                    in_stride=L, out_stride=so, fixed_aad_len=5))
