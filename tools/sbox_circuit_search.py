@@ -19,7 +19,11 @@ Each candidate is checked against the AES S-box on all 256 inputs before it
 is covered.  Output: one JSON line per candidate (seed, layer choice, cover
 size) and the best circuit.
 
-    python3 tools/sbox_circuit_search.py SEED COUNT [bottom|top|both] > log.jsonl
+    python3 tools/sbox_circuit_search.py SEED COUNT [bottom|top|both|none] [CIRCUIT] > log.jsonl
+
+CIRCUIT: bp113 (default; gen_bs_sbox.CIRCUIT), bp113r (with REASSOC, the
+shipped 72-gate start) or bpd16 (Boyar and Peralta's depth-16, 128-gate
+circuit, round 1's starting point); mode "none" covers the circuit as it is.
 """
 import json
 import os
@@ -28,6 +32,40 @@ import sys
 
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 import gen_bs_sbox as gb  # noqa: E402
+
+
+# Boyar and Peralta, "A depth-16 circuit for the AES S-box" (2011): 128
+# gates; S7..S0 here are output bits 7..0 (renamed below to this tool's
+# S0 = bit 7 convention), the four XNORs written as XORs like CIRCUIT.
+DEPTH16 = """
+T1=U0^U3 T2=U0^U5 T3=U0^U6 T4=U3^U5 T5=U4^U6 T6=T1^T5 T7=U1^U2 T8=U7^T6 T9=U7^T7 T10=T6^T7
+T11=U1^U5 T12=U2^U5 T13=T3^T4 T14=T6^T11 T15=T5^T11 T16=T5^T12 T17=T9^T16 T18=U3^U7 T19=T7^T18
+T20=T1^T19 T21=U6^U7 T22=T7^T21 T23=T2^T22 T24=T2^T10 T25=T20^T17 T26=T3^T16 T27=T1^T12
+M1=T13&T6 M2=T23&T8 M3=T14^M1 M4=T19&U7 M5=M4^M1 M6=T3&T16 M7=T22&T9 M8=T26^M6 M9=T20&T17
+M10=M9^M6 M11=T1&T15 M12=T4&T27 M13=M12^M11 M14=T2&T10 M15=M14^M11 M16=M3^M2 M17=M5^T24
+M18=M8^M7 M19=M10^M15 M20=M16^M13 M21=M17^M15 M22=M18^M13 M23=M19^T25 M24=M22^M23 M25=M22&M20
+M26=M21^M25 M27=M20^M21 M28=M23^M25 M29=M28&M27 M30=M26&M24 M31=M20&M23 M32=M27&M31 M33=M27^M25
+M34=M21&M22 M35=M24&M34 M36=M24^M25 M37=M21^M29 M38=M32^M33 M39=M23^M30 M40=M35^M36 M41=M38^M40
+M42=M37^M39 M43=M37^M38 M44=M39^M40 M45=M42^M41 M46=M44&T6 M47=M40&T8 M48=M39&U7 M49=M43&T16
+M50=M38&T9 M51=M37&T17 M52=M42&T15 M53=M45&T27 M54=M41&T10 M55=M44&T13 M56=M40&T23 M57=M39&T19
+M58=M43&T3 M59=M38&T22 M60=M37&T20 M61=M42&T1 M62=M45&T4 M63=M41&T2
+L0=M61^M62 L1=M50^M56 L2=M46^M48 L3=M47^M55 L4=M54^M58 L5=M49^M61 L6=M62^L5 L7=M46^L3 L8=M51^M59
+L9=M52^M53 L10=M53^L4 L11=M60^L2 L12=M48^M51 L13=M50^L0 L14=M52^M61 L15=M55^L1 L16=M56^L0
+L17=M57^L1 L18=M58^L8 L19=M63^L4 L20=L0^L1 L21=L1^L7 L22=L3^L12 L23=L18^L2 L24=L15^L9 L25=L6^L10
+L26=L7^L9 L27=L8^L10 L28=L11^L14 L29=L11^L17
+S7=L6^L24 S6=L16^L26 S5=L19^L28 S4=L6^L21 S3=L20^L22 S2=L25^L29 S1=L13^L27 S0=L6^L23
+"""
+
+
+def circuit(name):
+    if name == "bpd16":
+        g = gb.parse(DEPTH16)
+        ren = {"S%d" % k: "S%d" % (7 - k) for k in range(8)}   # S_k = bit k -> S_(7-k)
+        return {ren.get(n, n): (op, ren.get(a, a), ren.get(b, b)) for n, (op, a, b) in g.items()}
+    g = gb.parse(gb.CIRCUIT)
+    if name == "bp113r":
+        g.update(gb.parse(gb.REASSOC))
+    return g
 
 
 def lin_forms(gates, order, basis):
@@ -131,15 +169,14 @@ def rebuild(base_gates, layer, rng, eps):
 def main():
     seed, count = int(sys.argv[1]), int(sys.argv[2])
     mode = sys.argv[3] if len(sys.argv) > 3 else "bottom"
+    cname = sys.argv[4] if len(sys.argv) > 4 else ("bp113r" if os.environ.get("SBOX_FROM_REASSOC") else "bp113")
     rng = random.Random(seed)
-    base = gb.parse(gb.CIRCUIT)
-    if os.environ.get("SBOX_FROM_REASSOC"):
-        base.update(gb.parse(gb.REASSOC))
+    base = circuit(cname)
     best, best_g = None, None
     for it in range(count):
         g = base
         eps = rng.choice([0.0, 0.05, 0.15])
-        layers = ["bottom", "top"] if mode == "both" else [mode]
+        layers = ["bottom", "top"] if mode == "both" else [] if mode == "none" else [mode]
         for layer in layers:
             g = rebuild(g, layer, rng, eps)
         order = gb.topo(g)
@@ -147,7 +184,7 @@ def main():
         roots, res = gb.min_cover(g, order, time_limit=120)
         n = len(roots)
         xor2 = sum(1 for v in g.values() if v[0] == "^")
-        print(json.dumps({"seed": seed, "it": it, "mode": mode, "eps": eps, "xor2_gates": xor2,
+        print(json.dumps({"seed": seed, "it": it, "circuit": cname, "mode": mode, "eps": eps, "xor2_gates": xor2,
                           "and_gates": sum(1 for v in g.values() if v[0] == "&"),
                           "cover": n, "optimal": res.status == 0}), flush=True)
         if best is None or n < best:

@@ -8,6 +8,9 @@ annealing from that circuit (SBOX_FROM_REASSOC=1, seeds 21-24, uphill 0.25,
 ~75 minutes each) found nothing below 72.
 
     python3 tools/sbox_reassoc_search.py SEED STEPS [UPHILL] > gates.json
+
+SBOX_CIRCUIT=bpd16 starts from Boyar and Peralta's depth-16 circuit instead
+(tools/sbox_circuit_search.py circuit(); round 5).
 """
 import json
 import os
@@ -52,6 +55,9 @@ def main():
     cur = gb.parse(gb.CIRCUIT)
     if os.environ.get("SBOX_FROM_REASSOC"):   # continue from the shipped re-association
         cur.update(gb.parse(gb.REASSOC))
+    if os.environ.get("SBOX_CIRCUIT"):
+        import sbox_circuit_search as scs
+        cur = scs.circuit(os.environ["SBOX_CIRCUIT"])
     best = cover_size(cur)
     print("start %d" % best, file=sys.stderr, flush=True)
     # annealing: a cover one gate larger is accepted with probability ``uphill``
