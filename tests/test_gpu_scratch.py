@@ -1,7 +1,7 @@
 """GPU: the per-launch scratch of the hybrid AES-GCM kernel (job counter,
-batch copy and the per-record keystream masks) is stream-ordered memory from
-the device pool, freed behind each launch: batches launched on
-many short-lived streams leave device memory flat, and their records stay
+batch copy and the per-record keystream masks) comes from the library's
+scratch cache and goes back behind each launch: batches
+launched on many streams leave device memory flat, and their records stay
 right."""
 import numpy as np
 import pytest
@@ -34,7 +34,7 @@ def test_many_streams_memory_flat(oracle_mod):
     # before the count starts; then one AES-GCM batch per stream.
     chacha = tlsgpu.HipCHACHA20_POLY1305(bytearray(32))
     streams = [torch.cuda.Stream() for _ in range(40)]
-    tlsgpu.seal_batch(obj, b)                 # the pool's first block
+    tlsgpu.seal_batch(obj, b)                 # the cache's first buffer
     for st in streams:
         tlsgpu.seal_batch(chacha, b, st)
     torch.cuda.synchronize()

@@ -77,7 +77,7 @@ __device__ __forceinline__ void ccm_mac_head(Step&& step, uint4 nv, uint32_t a1,
     }
 }
 
-template <int NR, bool OPEN, int TAG, bool WIN, class RK>
+template <int NR, bool OPEN, int TAG, bool WIN, class RK, int G = 0>
 __device__ __forceinline__ void ccm_record(const tg_batch& b, uint64_t i, uint32_t lane4,
                                            const RK& rk) {
     const uint8_t* in = rec_in(b, i);
@@ -108,8 +108,8 @@ __device__ __forceinline__ void ccm_record(const tg_batch& b, uint64_t i, uint32
     uint4 wc = win_consts_w<NR>(lane4, rk, cc, a3);
     uint32_t whi = 0;
     uint4 ks = aes_ctr_win<NR>(lane4, rk, cc, wc, 1u);
-    for (uint32_t j = 0; j < nfull; ++j) {
-        const uint4 d = load16(in + 16 * j, aligned);
+    // one block of the loop: XOR, store, MAC step, the next block's keystream
+    auto step = [&](uint32_t j, const uint4& d) {
         const uint4 c = xor4(d, ks);
         store16(out + 16 * j, c, aligned);
         // next block's keystream is independent of this block's CBC step
@@ -123,7 +123,28 @@ __device__ __forceinline__ void ccm_record(const tg_batch& b, uint64_t i, uint32
             ks = aes_ctr_win<NR>(lane4, rk, cc, wc, j + 2u);
         }
         x = aes_block<NR>(lane4, rk, xor_blk(x, OPEN ? c : d));
+    };
+    // the payload G blocks at a time, the next group's loads issued before
+    // this group's blocks run (G = 0: a dependent load per block)
+    uint32_t j = 0;
+    if (G > 0 && nfull >= (uint32_t)G) {
+        uint4 d[G > 0 ? G : 1];
+#pragma unroll
+        for (int q = 0; q < G; ++q) d[q] = load16(in + 16 * q, aligned);
+        for (; j + 2 * G <= nfull; j += G) {
+            uint4 nx[G > 0 ? G : 1];
+#pragma unroll
+            for (int q = 0; q < G; ++q) nx[q] = load16(in + 16 * (j + G + q), aligned);
+#pragma unroll
+            for (int q = 0; q < G; ++q) step(j + q, d[q]);
+#pragma unroll
+            for (int q = 0; q < G; ++q) d[q] = nx[q];
+        }
+#pragma unroll
+        for (int q = 0; q < G; ++q) step(j + q, d[q]);
+        j += G;
     }
+    for (; j < nfull; ++j) step(j, load16(in + 16 * j, aligned));
     if (tail) {
         const uint4 d = load_partial(in + 16 * nfull, tail);
         const uint4 c = mask_tail(xor4(d, ks), tail);
@@ -155,8 +176,11 @@ __device__ __forceinline__ void ccm_record(const tg_batch& b, uint64_t i, uint32
 // WIN: the keystream through the 256-counter window cache (default);
 // option ccm_variant 1 runs full rounds (measurement).  A key-table record
 // whose key_idx is not below nkeys is skipped (open: status 0).
-template <int NR, bool OPEN, int TAG, bool TABLE, bool WIN>
-__global__ __launch_bounds__(ccm_threads<TABLE>()) void ccm_kernel(const AesKeyDev* __restrict__ keys,
+// Single key: two 1024-thread workgroups per CU (64 KiB of Te each) need <= 64
+// VGPRs (8 waves per SIMD, HIP's second launch bound), so the one-block
+// prefetch (G = 1) is held to that; deeper prefetch takes one workgroup per CU.
+template <int NR, bool OPEN, int TAG, bool TABLE, bool WIN, int G = 0>
+__global__ __launch_bounds__(ccm_threads<TABLE>(), (!TABLE && G <= 1) ? 8 : 1) void ccm_kernel(const AesKeyDev* __restrict__ keys,
                                                           uint64_t nkeys, tg_batch b) {
     stage_te(reinterpret_cast<uint32_t*>(g_lds_ccm));   // Te0/Te2 copies at LDS 0
     __syncthreads();
@@ -171,7 +195,7 @@ __global__ __launch_bounds__(ccm_threads<TABLE>()) void ccm_kernel(const AesKeyD
 #pragma unroll
     for (int k = 0; k < 4 * (NR + 1); ++k) rk.w[k] = kp->rk[k];
     const uint32_t lane4 = (threadIdx.x & 31u) << 2;
-    ccm_record<NR, OPEN, TAG, WIN>(b, i, lane4, rk);
+    ccm_record<NR, OPEN, TAG, WIN, RkRegs<NR>, G>(b, i, lane4, rk);
 }
 
 // ---- one block on the four lanes of a quad (the serial CBC-MAC chain) ----
@@ -635,7 +659,7 @@ int launch_hy(const AesKeyDev* key, const tg_batch& b, hipStream_t s) {
                            reinterpret_cast<const uint4*>(scratch + 128), scratch, nt);
         rc = hipGetLastError() == hipSuccess ? TG_OK : TG_EHIP;
     }
-    if (hipFreeAsync(scratch, s) != hipSuccess && !rc) rc = TG_EHIP;
+    if (stream_free(scratch, s) && !rc) rc = TG_EHIP;
     return rc;
 }
 
@@ -653,13 +677,13 @@ int launch_wave(const AesKeyDev* keys, uint64_t nkeys, const tg_batch& b, hipStr
 // kernels meet near 4096 records: profiles/r02/v22_ccm_wave.txt).
 constexpr uint64_t kCcmWaveMaxRecords = 4096;
 
-template <int NR, bool OPEN, int TAG, bool TABLE, bool WIN>
+template <int NR, bool OPEN, int TAG, bool TABLE, bool WIN, int G = 0>
 int launch_w(const AesKeyDev* keys, uint64_t nkeys, const tg_batch& b, hipStream_t s) {
-    if (lds_attr((const void*)ccm_kernel<NR, OPEN, TAG, TABLE, WIN>, (int)kCcmLds)) return TG_EHIP;
+    if (lds_attr((const void*)ccm_kernel<NR, OPEN, TAG, TABLE, WIN, G>, (int)kCcmLds)) return TG_EHIP;
     constexpr int threads = ccm_threads<TABLE>();
     const uint64_t blocks = (b.n + threads - 1) / threads;
     if (blocks > 0x7fffffffull) return TG_EINVAL;
-    hipLaunchKernelGGL((ccm_kernel<NR, OPEN, TAG, TABLE, WIN>), dim3((unsigned)blocks),
+    hipLaunchKernelGGL((ccm_kernel<NR, OPEN, TAG, TABLE, WIN, G>), dim3((unsigned)blocks),
                        dim3(threads), kCcmLds, s, keys, nkeys, b);
     return hipGetLastError() == hipSuccess ? TG_OK : TG_EHIP;
 }
@@ -667,7 +691,8 @@ int launch_w(const AesKeyDev* keys, uint64_t nkeys, const tg_batch& b, hipStream
 // Option ccm_variant (tests and measurement): 0 = auto (wave per record up
 // to kCcmWaveMaxRecords, else lane per record with the window cache), 1 =
 // lane per record, full rounds, 2 = wave per record, 3 = lane per record
-// with the window cache, 4 = the hybrid lane-per-record kernel (single key).
+// with the window cache, 4 = the hybrid lane-per-record kernel (single key),
+// 5 / 6 / 7 = 3 with the payload loaded 1 / 2 / 4 blocks ahead.
 template <int NR, bool OPEN, int TAG, bool TABLE>
 int launch(const AesKeyDev* keys, uint64_t nkeys, const tg_batch& b, hipStream_t s) {
     switch (opt(kOptCcmVariant)) {
@@ -680,6 +705,9 @@ int launch(const AesKeyDev* keys, uint64_t nkeys, const tg_batch& b, hipStream_t
         case 4:
             if (TABLE) return launch_w<NR, OPEN, TAG, TABLE, true>(keys, nkeys, b, s);
             return launch_hy<NR, OPEN, TAG>(keys, b, s);
+        case 5: return launch_w<NR, OPEN, TAG, TABLE, true, 1>(keys, nkeys, b, s);
+        case 6: return launch_w<NR, OPEN, TAG, TABLE, true, 2>(keys, nkeys, b, s);
+        case 7: return launch_w<NR, OPEN, TAG, TABLE, true, 4>(keys, nkeys, b, s);
         default: return TG_EINVAL;
     }
 }

@@ -675,12 +675,12 @@ int launch_hy(const GcmKeyDev* key, const tg_batch& b, hipStream_t s, const uint
     const void* fn = small ? (const void*)gcm_hy_kernel<NR, OPEN, 768> : (const void*)gcm_hy_kernel<NR, OPEN, 1024>;
     if (lds_attr(fn, (int)kHyLds)) return TG_EHIP;
     // The launch's scratch -- job counter and batch copy (256 bytes), then two
-    // 16-byte keystream blocks per record (hy_mask_kernel) -- is allocated
-    // stream-ordered from the device's memory pool (stream_alloc: the pool
-    // keeps freed memory, so this is a host-side bookkeeping step, not a
-    // device allocation) and freed behind the kernel: nothing outlives the
-    // call, and launches on different streams (hipStreamPerThread included)
-    // never share it.  The key rows and rotated round keys come
+    // 16-byte keystream blocks per record (hy_mask_kernel) -- comes from the
+    // per-launch scratch cache (api.hip stream_alloc: a buffer is reused once
+    // the launches behind it have completed, or at once on the same stream)
+    // and goes back behind the kernel: launches on different streams
+    // (hipStreamPerThread included) never share it, and memory is bounded by
+    // the launches in flight.  The key rows and rotated round keys come
     // with the key (GcmKeyDev::bs8rows, rkrot).
 #if defined(TG_HY_NO_MASK)   // A/B builds: every wave computes its records' masks
     const uint64_t mrec = 0;
@@ -695,7 +695,7 @@ int launch_hy(const GcmKeyDev* key, const tg_batch& b, hipStream_t s, const uint
     hipLaunchKernelGGL(hy_setup_kernel, dim3(1), dim3(64), 0, s, b, queue, bcopy);
     int rc = hipGetLastError() == hipSuccess ? TG_OK : TG_EHIP;
     if (!rc) rc = launch_hy_kernels<NR, OPEN>(key, b, s, order, nt, prio, small, queue, bcopy, masks);
-    if (hipFreeAsync(scratch, s) != hipSuccess && !rc) rc = TG_EHIP;
+    if (stream_free(scratch, s) && !rc) rc = TG_EHIP;
     return rc;
 }
 
@@ -1035,7 +1035,7 @@ int launch_kt(const GcmTableKey* keys, uint64_t nkeys, const uint4* hpow, const 
         }
     }
     if (!rc) rc = tg_launch_gcm_table_lane(keys, nkeys, NR, b, OPEN, s, order, nlong);
-    if (hipFreeAsync(buf, s) != hipSuccess) return TG_EHIP;
+    if (stream_free(buf, s)) return TG_EHIP;
     return rc;
 }
 

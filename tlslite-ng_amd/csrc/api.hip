@@ -261,9 +261,9 @@ int launch_gcm_table(tg_key* k, const tg_batch& b, bool open, hipStream_t s) {
                             split, lpr, hybrid);
 }
 
-// The order and the sort's scratch are allocated stream-ordered on the
-// launch's stream (hipMallocAsync / hipFreeAsync), so batches in flight on
-// other streams never share them.
+// The order and the sort's scratch come from the per-launch scratch cache
+// (stream_alloc / stream_free), so batches in flight on other streams never
+// share them.
 int launch(tg_key* k, const tg_batch& b, bool open, hipStream_t s) {
     if (is_ccm(k->alg))
         return tg_launch_ccm(static_cast<const tg::AesKeyDev*>(k->dev_key), k->nkeys, k->rounds, k->taglen,
@@ -283,7 +283,7 @@ int launch(tg_key* k, const tg_batch& b, bool open, hipStream_t s) {
     uint32_t* order = reinterpret_cast<uint32_t*>(buf);
     rc = tg_length_order(b.len, b.n, order, buf + obytes, &scratch, s);
     if (!rc) rc = launch_kernels(k, b, open, s, order);
-    (void)hipFreeAsync(buf, s);
+    (void)tg::stream_free(buf, s);
     return rc;
 }
 
@@ -384,7 +384,7 @@ struct ScratchAlloc {
     void* base = nullptr;
     hipStream_t s = nullptr;
     ~ScratchAlloc() {
-        if (base) (void)hipFreeAsync(base, s);
+        if (base) (void)tg::stream_free(base, s);
     }
 };
 
@@ -536,22 +536,73 @@ int lds_attr(const void* fn, int bytes) {
     return TG_OK;
 }
 
+// Per-launch scratch (common.h stream_alloc / stream_free): a process-wide
+// list of device buffers, each free for reuse once the event recorded behind
+// its last launch has completed.  A buffer released on a stream is taken
+// again at once only by the next launch on that same stream (stream order
+// protects it) -- never through hipStreamPerThread or the null stream, whose
+// handle names a different stream in each thread.  So memory is bounded by
+// the launches in flight, not by the streams a caller has ever used, and
+// nothing is keyed on a stream handle.  (The device memory
+// pool of hipMallocAsync measured 4.7 MB more per stream used, without
+// reuse across streams: profiles/r05/r5b.)
+namespace {
+struct ScratchBuf {
+    void* p = nullptr;
+    size_t cap = 0;
+    int dev = -1;
+    hipEvent_t done = nullptr;   // recorded behind the buffer's last launch
+    hipStream_t last = nullptr;  // the stream of that launch
+    bool busy = false;           // between stream_alloc and stream_free
+};
+std::mutex g_scratch_mu;
+std::vector<ScratchBuf>& scratch_list() {
+    static std::vector<ScratchBuf>* v = new std::vector<ScratchBuf>();   // outlives static teardown
+    return *v;
+}
+bool per_thread_handle(hipStream_t s) { return s == nullptr || s == hipStreamPerThread; }
+}  // namespace
+
 int stream_alloc(void** p, size_t bytes, hipStream_t s) {
-    static std::mutex mu;
-    static std::set<int> pools;   // devices whose default pool keeps its memory
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess) return TG_EHIP;
-    {
-        std::lock_guard<std::mutex> g(mu);
-        if (!pools.count(dev)) {
-            hipMemPool_t pool = nullptr;
-            if (hipDeviceGetDefaultMemPool(&pool, dev) != hipSuccess) return TG_EHIP;
-            uint64_t keep = ~0ull;
-            if (hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &keep) != hipSuccess) return TG_EHIP;
-            pools.insert(dev);
+    if (!bytes) bytes = 1;
+    std::lock_guard<std::mutex> g(g_scratch_mu);
+    auto& v = scratch_list();
+    ScratchBuf* pick = nullptr;
+    for (auto& b : v) {
+        if (b.busy || b.dev != dev || b.cap < bytes) continue;
+        const bool ordered = b.last == s && !per_thread_handle(s);
+        if (ordered || !b.done || hipEventQuery(b.done) == hipSuccess) {
+            if (!pick || b.cap < pick->cap) pick = &b;
         }
     }
-    return hipMallocAsync(p, bytes ? bytes : 1, s) == hipSuccess ? TG_OK : TG_EHIP;
+    if (!pick) {
+        ScratchBuf nb;
+        nb.cap = bytes < (1u << 20) ? (size_t)1 << 20 : (bytes + 0xfffff) & ~(size_t)0xfffff;
+        nb.dev = dev;
+        if (hipMalloc(&nb.p, nb.cap) != hipSuccess) return TG_EHIP;
+        if (hipEventCreateWithFlags(&nb.done, hipEventDisableTiming) != hipSuccess) {
+            (void)hipFree(nb.p);
+            return TG_EHIP;
+        }
+        v.push_back(nb);
+        pick = &v.back();
+    }
+    pick->busy = true;
+    *p = pick->p;
+    return TG_OK;
+}
+
+int stream_free(void* p, hipStream_t s) {
+    std::lock_guard<std::mutex> g(g_scratch_mu);
+    for (auto& b : scratch_list()) {
+        if (b.p != p) continue;
+        b.busy = false;
+        b.last = s;
+        return hipEventRecord(b.done, s) == hipSuccess ? TG_OK : TG_EHIP;
+    }
+    return TG_EINVAL;
 }
 
 // tg_version()'s text; a measurement build appends its flags (common.h).

@@ -284,13 +284,14 @@ __host__ __device__ constexpr bool lone_last_block(uint32_t nc) {
 // device, once per (function, device); thread-safe (api.hip).  0 or TG_EHIP.
 int lds_attr(const void* fn, int bytes);
 
-// Stream-ordered scratch (hipMallocAsync on ``s``) from the current device's
-// default memory pool, whose release threshold is raised to "keep
-// everything" on first use per device: a freed block (hipFreeAsync) stays in
-// the pool for the next launch, so per-launch scratch costs host bookkeeping
-// and no device allocation, and nothing outlives its launch (api.hip).
-// 0 or TG_EHIP.
+// Per-launch device scratch for launches on stream ``s``: stream_alloc takes
+// a buffer of at least ``bytes`` from a process-wide cache (reused once the
+// launches that last used it have completed, or at once by the next launch
+// on the same stream), stream_free hands it back behind the work queued on
+// ``s`` (api.hip).  0, TG_EHIP, or TG_EINVAL for a pointer not from
+// stream_alloc.
 int stream_alloc(void** p, size_t bytes, hipStream_t s);
+int stream_free(void* p, hipStream_t s);
 
 // Compute units of the current device (grid size of the persistent kernels),
 // looked up once per device.

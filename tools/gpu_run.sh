@@ -62,7 +62,13 @@ for st0 in "$@"; do
       find $O/prof -name "*kernel_stats.csv" -exec cp {} $O/kernel_stats.csv \;
       head -12 $O/kernel_stats.csv ;;
     pmc)
-      bash tools/pmc_full.sh $T ;;
+      bash tools/pmc_full.sh $T/pmc ;;
+    fetch)   # FETCH_SIZE / WRITE_SIZE of one seal + open per PROF_ALGS AEAD (2^18 x 16 KiB)
+      for c in FETCH_SIZE WRITE_SIZE; do
+        (cd /tmp && export TMPDIR=/tmp && timeout -k 10 180 rocprofv3 --pmc $c --kernel-trace --stats --output-format csv \
+          -d $O/fetch_$c$SUF -o pass -- python3 $R/tools/prof_kernels.py > $O/fetch_$c$SUF.log 2>&1)
+      done
+      python3 tools/pmc_summary.py $O > $O/fetch$SUF.txt 2>&1 || true; head -40 $O/fetch$SUF.txt ;;
     traffic)
       bash tools/traffic.sh $T ;;
     ab=*)
