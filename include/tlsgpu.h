@@ -287,6 +287,11 @@ int tg_selftest_ghash(int mode, const uint8_t* h, const uint8_t* aad, const uint
                       const uint32_t* aad_len, const uint8_t* ct, const uint64_t* ct_off,
                       const uint32_t* ct_len, uint64_t n, uint8_t* out);
 
+/* Diagnostics: the per-launch scratch the library holds (the buffers of
+ * its scratch cache, all devices) -- bounded by the launches in flight, not
+ * by the streams a caller has used.  Test and monitoring use. */
+int tg_scratch_info(uint64_t* bytes, uint64_t* buffers);
+
 /* Device memory helpers so a ctypes host needs no other GPU runtime. */
 int tg_malloc(void** p, size_t bytes);
 int tg_free(void* p);

@@ -594,6 +594,13 @@ int stream_alloc(void** p, size_t bytes, hipStream_t s) {
     return TG_OK;
 }
 
+void scratch_totals(uint64_t* bytes, uint64_t* buffers) {
+    std::lock_guard<std::mutex> g(g_scratch_mu);
+    *bytes = 0;
+    *buffers = scratch_list().size();
+    for (const auto& b : scratch_list()) *bytes += b.cap;
+}
+
 int stream_free(void* p, hipStream_t s) {
     std::lock_guard<std::mutex> g(g_scratch_mu);
     for (auto& b : scratch_list()) {
@@ -890,6 +897,12 @@ int tg_gather(const uint8_t* src, const uint64_t* src_off, const uint32_t* len, 
     if (n == 0) return TG_OK;
     int rc = tg_launch_gather(src, src_off, len, dst, dst_off, n, static_cast<hipStream_t>(stream));
     return rc ? fail(rc, "gather kernel launch failed") : TG_OK;
+}
+
+int tg_scratch_info(uint64_t* bytes, uint64_t* buffers) {
+    if (!bytes || !buffers) return fail(TG_EINVAL, "null argument");
+    tg::scratch_totals(bytes, buffers);
+    return TG_OK;
 }
 
 int tg_stream_sync(void* stream) {

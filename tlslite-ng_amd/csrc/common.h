@@ -292,6 +292,7 @@ int lds_attr(const void* fn, int bytes);
 // stream_alloc.
 int stream_alloc(void** p, size_t bytes, hipStream_t s);
 int stream_free(void* p, hipStream_t s);
+void scratch_totals(uint64_t* bytes, uint64_t* buffers);   // tg_scratch_info
 
 // Compute units of the current device (grid size of the persistent kernels),
 // looked up once per device.

@@ -31,7 +31,8 @@ EXPORTS = ("tg_version", "tg_last_error", "tg_device_count", "tg_init", "tg_key_
            "tg_open_batch", "tg_make_nonces", "tg_malloc", "tg_free", "tg_memcpy_h2d",
            "tg_memcpy_d2h", "tg_stream_sync", "tg_seal_records", "tg_open_records",
            "tg_hkdf_expand_label", "tg_key_create_device", "tg_scan_records", "tg_gather",
-           "tg_selftest_poly1305", "tg_selftest_ghash", "tg_set_option", "tg_get_option")
+           "tg_selftest_poly1305", "tg_selftest_ghash", "tg_set_option", "tg_get_option",
+           "tg_scratch_info")
 
 TG_TLS12 = 0x0303
 TG_TLS13 = 0x0304
@@ -138,6 +139,7 @@ def load():
     l.tg_selftest_ghash.argtypes = [i, p, p, p, p, p, p, p, u64, p]
     l.tg_set_option.argtypes = [ctypes.c_char_p, i]
     l.tg_get_option.argtypes = [ctypes.c_char_p, ctypes.POINTER(ctypes.c_int)]
+    l.tg_scratch_info.argtypes = [ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64)]
     for name in EXPORTS:
         if name not in ("tg_version", "tg_last_error"):
             getattr(l, name).restype = ctypes.c_int
@@ -191,6 +193,13 @@ class options(object):
         for k, v in self.old.items():
             set_option(k, v)
         return False
+
+
+def scratch_info():
+    """(bytes, buffers) of per-launch scratch the library holds (tg_scratch_info)."""
+    b, n = ctypes.c_uint64(0), ctypes.c_uint64(0)
+    check(load().tg_scratch_info(ctypes.byref(b), ctypes.byref(n)))
+    return b.value, n.value
 
 
 def device_count():

@@ -123,10 +123,18 @@ def rebuild(base_gates, layer, rng, eps):
     g = dict(base_gates)
     order = gb.topo(g)
     if layer == "bottom":
-        basis = ["Z%d" % i for i in range(18)]
+        # the products that only XORs follow (BP113's Z0..Z17, depth-16's M46..M63)
+        users = {}
+        for n, (op, a, c) in g.items():
+            users.setdefault(a, []).append(n)
+            users.setdefault(c, []).append(n)
+
+        def xor_only(n):
+            return all(g[u][0] == "^" and xor_only(u) for u in users.get(n, []))
+        basis = sorted((n for n, v in g.items() if v[0] == "&" and xor_only(n)), key=gb.key)
         f = lin_forms(g, order, basis)
         targets = {"S%d" % i: f["S%d" % i] for i in range(8)}
-        drop = [n for n in g if n in f and n not in basis and not n.startswith("Z")]
+        drop = [n for n in g if n in f and n not in basis]
     else:   # top: every XOR-only function of U0..U7 that the rest of the circuit reads
         basis = gb.INPUTS
         f = lin_forms(g, order, basis)
