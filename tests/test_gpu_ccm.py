@@ -95,8 +95,8 @@ LEN_MIX = [0, 1, 15, 16, 17, 31, 63, 64, 65, 100, 255, 256, 1000, 1024, 1025, 40
 @pytest.mark.parametrize("align", [16, 1])
 # auto / lane full rounds / wave per record / lane counter-window cache /
 # hybrid (bitsliced keystream + T-table MAC; "4t": T-table waves only, "4b":
-# bitsliced-keystream waves only) / lane with the payload 1 / 2 / 4 blocks ahead
-@pytest.mark.parametrize("variant", ["0", "1", "2", "3", "4", "4t", "4b", "5", "6", "7"])
+# bitsliced-keystream waves only) / lane with the payload 1 / 2 / 4 / 8 blocks ahead
+@pytest.mark.parametrize("variant", ["0", "1", "2", "3", "4", "4t", "4b", "5", "6", "7", "8"])
 def test_batch_ragged_vs_oracle(torch, tg, oracle_mod, klen, tl, align, variant):
     from batchpack import HostBatch, run_seal_open
     rng = np.random.default_rng(klen * 11 + tl + align)

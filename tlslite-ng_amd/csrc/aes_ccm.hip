@@ -620,7 +620,7 @@ __global__ __launch_bounds__(kCcmHyThreads) void ccm_hy_kernel(const AesKeyDev* 
         const uint64_t i = 64ull * job + (threadIdx.x & 63u);
         const bool valid = i < b.n;
         if (wave < nt) {
-            if (valid) ccm_record<NR, OPEN, TAG, true>(b, i, lane4, rk);
+            if (valid) ccm_record<NR, OPEN, TAG, true, RkLds, 4>(b, i, lane4, rk);
         } else {
             ccm_bs_record<NR, OPEN, TAG>(b, i, valid, lane4, rk, bs8::KeyPlanesVmemFolded{{krows}}, rows);
         }
@@ -692,7 +692,7 @@ int launch_w(const AesKeyDev* keys, uint64_t nkeys, const tg_batch& b, hipStream
 // to kCcmWaveMaxRecords, else lane per record with the window cache), 1 =
 // lane per record, full rounds, 2 = wave per record, 3 = lane per record
 // with the window cache, 4 = the hybrid lane-per-record kernel (single key),
-// 5 / 6 / 7 = 3 with the payload loaded 1 / 2 / 4 blocks ahead.
+// 5 / 6 / 7 / 8 = 3 with the payload loaded 1 / 2 / 4 / 8 blocks ahead.
 template <int NR, bool OPEN, int TAG, bool TABLE>
 int launch(const AesKeyDev* keys, uint64_t nkeys, const tg_batch& b, hipStream_t s) {
     switch (opt(kOptCcmVariant)) {
@@ -708,6 +708,7 @@ int launch(const AesKeyDev* keys, uint64_t nkeys, const tg_batch& b, hipStream_t
         case 5: return launch_w<NR, OPEN, TAG, TABLE, true, 1>(keys, nkeys, b, s);
         case 6: return launch_w<NR, OPEN, TAG, TABLE, true, 2>(keys, nkeys, b, s);
         case 7: return launch_w<NR, OPEN, TAG, TABLE, true, 4>(keys, nkeys, b, s);
+        case 8: return launch_w<NR, OPEN, TAG, TABLE, true, 8>(keys, nkeys, b, s);
         default: return TG_EINVAL;
     }
 }

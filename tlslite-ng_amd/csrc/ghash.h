@@ -284,6 +284,35 @@ __device__ __forceinline__ void build_table4(uint32_t tab, uint4 gn) {
     bas[1] = gf128_mulx(bas[0]);
     bas[2] = gf128_mulx(bas[1]);
     bas[3] = gf128_mulx(bas[2]);
+#if defined(TG_BUILD_ROT)
+    // entry n0 + (n + j) % 8 at step n: the 8 lanes of a ds_write_b128 group
+    // write 8 different bank slots instead of one (an 8-way conflict)
+    uint4 e[8];
+#pragma unroll
+    for (uint32_t n = 0; n < 8; ++n) {
+        const uint32_t nn = n0 + n;
+        uint4 v = make_uint4(0, 0, 0, 0);
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+            if (nn & (8u >> k)) v = xor4(v, bas[k]);
+        e[n] = norm4(v);
+    }
+    // rotate the eight entries by j % 8 (three stages of per-lane selects)
+#pragma unroll
+    for (int st = 1; st < 8; st <<= 1) {
+        const bool sw = (j & (uint32_t)st) != 0;
+        uint4 t[8];
+#pragma unroll
+        for (int n = 0; n < 8; ++n) {
+            const uint4 a = e[n], b = e[(n + st) & 7];
+            t[n] = make_uint4(sw ? b.x : a.x, sw ? b.y : a.y, sw ? b.z : a.z, sw ? b.w : a.w);
+        }
+#pragma unroll
+        for (int n = 0; n < 8; ++n) e[n] = t[n];
+    }
+#pragma unroll
+    for (uint32_t n = 0; n < 8; ++n) lds_st128(tab + 256u * j + 16u * (n0 + ((n + j) & 7u)), e[n]);
+#else
 #pragma unroll
     for (uint32_t n = 0; n < 8; ++n) {
         const uint32_t nn = n0 + n;
@@ -293,6 +322,7 @@ __device__ __forceinline__ void build_table4(uint32_t tab, uint4 gn) {
             if (nn & (8u >> k)) v = xor4(v, bas[k]);
         lds_st128(tab + 256u * j + 16u * nn, norm4(v));
     }
+#endif
 }
 
 // y * G through the 4-bit tables at ``tab`` (32 lookups, no reduction).
