@@ -698,6 +698,11 @@ int launch(const AesKeyDev* keys, uint64_t nkeys, const tg_batch& b, hipStream_t
     switch (opt(kOptCcmVariant)) {
         case 0:
             if (b.n <= kCcmWaveMaxRecords) return launch_wave<NR, OPEN, TAG, TABLE>(keys, nkeys, b, s);
+            // single key: the payload four blocks ahead (one 1024-thread
+            // workgroup per CU at 95 VGPRs): 612 against 502 GiB/s for the
+            // dependent load per block at two workgroups per CU
+            // (profiles/r05/r5d, r5e; 2 / 8 blocks: 604 / 589)
+            if (!TABLE) return launch_w<NR, OPEN, TAG, TABLE, true, 4>(keys, nkeys, b, s);
             return launch_w<NR, OPEN, TAG, TABLE, true>(keys, nkeys, b, s);
         case 1: return launch_w<NR, OPEN, TAG, TABLE, false>(keys, nkeys, b, s);
         case 2: return launch_wave<NR, OPEN, TAG, TABLE>(keys, nkeys, b, s);

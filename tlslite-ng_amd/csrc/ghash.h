@@ -284,9 +284,10 @@ __device__ __forceinline__ void build_table4(uint32_t tab, uint4 gn) {
     bas[1] = gf128_mulx(bas[0]);
     bas[2] = gf128_mulx(bas[1]);
     bas[3] = gf128_mulx(bas[2]);
-#if defined(TG_BUILD_ROT)
     // entry n0 + (n + j) % 8 at step n: the 8 lanes of a ds_write_b128 group
-    // write 8 different bank slots instead of one (an 8-way conflict)
+    // (8 consecutive lanes, banks (a / 4) mod 32) write 8 different bank
+    // slots instead of one -- an 8-way conflict on every store; config 4
+    // +0.7 %, two of two rounds on one box (profiles/r05/r5e/)
     uint4 e[8];
 #pragma unroll
     for (uint32_t n = 0; n < 8; ++n) {
@@ -312,17 +313,6 @@ __device__ __forceinline__ void build_table4(uint32_t tab, uint4 gn) {
     }
 #pragma unroll
     for (uint32_t n = 0; n < 8; ++n) lds_st128(tab + 256u * j + 16u * (n0 + ((n + j) & 7u)), e[n]);
-#else
-#pragma unroll
-    for (uint32_t n = 0; n < 8; ++n) {
-        const uint32_t nn = n0 + n;
-        uint4 v = make_uint4(0, 0, 0, 0);
-#pragma unroll
-        for (int k = 0; k < 4; ++k)
-            if (nn & (8u >> k)) v = xor4(v, bas[k]);
-        lds_st128(tab + 256u * j + 16u * nn, norm4(v));
-    }
-#endif
 }
 
 // y * G through the 4-bit tables at ``tab`` (32 lookups, no reduction).
