@@ -95,9 +95,8 @@ LEN_MIX = [0, 1, 15, 16, 17, 31, 63, 64, 65, 100, 255, 256, 1000, 1024, 1025, 40
 @pytest.mark.parametrize("align", [16, 1])
 # auto / lane full rounds / wave per record / lane counter-window cache /
 # hybrid (bitsliced keystream + T-table MAC; "4t": T-table waves only, "4b":
-# bitsliced-keystream waves only) / lane with the payload 1 / 2 / 4 / 8 blocks ahead /
-# split keystream || MAC kernels
-@pytest.mark.parametrize("variant", ["0", "1", "2", "3", "4", "4t", "4b", "5", "6", "7", "8", "9"])
+# bitsliced-keystream waves only) / lane with the payload 1 / 2 / 4 / 8 blocks ahead
+@pytest.mark.parametrize("variant", ["0", "1", "2", "3", "4", "4t", "4b", "5", "6", "7", "8"])
 def test_batch_ragged_vs_oracle(torch, tg, oracle_mod, klen, tl, align, variant):
     from batchpack import HostBatch, run_seal_open
     rng = np.random.default_rng(klen * 11 + tl + align)
@@ -164,28 +163,25 @@ def test_batch_fixtures(torch, tg, bi):
 
 @pytest.mark.parametrize("klen,tl", [(16, 16), (16, 8), (32, 16)])
 def test_hybrid_counter_past_2_16(torch, tg, oracle_mod, klen, tl):
-    """Bitsliced keystreams (hybrid kernel, split keystream kernel) of
-    records over 1 MiB: counters from 2^16 on change rows 0-1 of the counter
-    block, so the bitsliced batches leave the per-record round-1 cache
-    (aesccm.py:72-83 counter layout)."""
+    """Hybrid kernel records over 1 MiB: counters from 2^16 on change rows
+    0-1 of the counter block, so the bitsliced batches leave the per-record
+    round-1 cache (aesccm.py:72-83 counter layout)."""
     from batchpack import HostBatch, run_seal_open
     rng = np.random.default_rng(77 + tl + klen)
     lens = [1 << 20, (1 << 20) + 16, (1 << 20) + 1000, 1100007] + list(rng.integers(0, 3000, 60))
     hb = HostBatch(lens, payload_seed=6, align=16, aad_mode="tls13", tag=tl)
     key = rng.bytes(klen)
-    for opts in ({"ccm_variant": 4, "ccm_hy_t": -1}, {"ccm_variant": 9}):
-        with tg.options(**opts):
-            run_seal_open(torch, tg, oracle_mod, hb, "aesccm" if tl == 16 else "aesccm8",
-                          np.frombuffer(key, np.uint8), _obj(tg, key, tl), tamper=(1, 7))
+    with tg.options(ccm_variant=4, ccm_hy_t=-1):
+        run_seal_open(torch, tg, oracle_mod, hb, "aesccm" if tl == 16 else "aesccm8",
+                      np.frombuffer(key, np.uint8), _obj(tg, key, tl), tamper=(1, 7))
 
 
-@pytest.mark.parametrize("variant", [0, 4, 9])
+@pytest.mark.parametrize("variant", [0, 4])
 def test_large_roundtrip_and_samples(torch, tg, oracle_mod, variant):
     """2^18 x 16 KiB AES-128-CCM records: seal -> open round trip, every
     record's ciphertext and tag against the threaded C oracle
     (tests/fullcheck.py), and 32 sampled records through its per-record
-    entry point; variant 4 forces the hybrid kernel, 9 the split keystream ||
-    MAC kernels (open in chunks of 2^17 records)."""
+    entry point; variant 4 forces the hybrid kernel."""
     with tg.options(ccm_variant=variant):
         _large(torch, tg, oracle_mod)
 

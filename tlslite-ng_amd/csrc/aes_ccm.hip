@@ -27,9 +27,6 @@
 // 128-bit increment would carry into the nonce (tlsgpu.h documents the limit).
 #include <stdlib.h>
 
-#include <mutex>
-#include <vector>
-
 #include "aes_bs8.h"
 #include "aes_round.h"
 #include "options.h"
@@ -465,9 +462,7 @@ __device__ __forceinline__ uint4 aes_block_rolled(uint32_t lane4, const RK& rkp,
                       col_last(s2, s3, s0, s1, k.z, lane4), col_last(s3, s0, s1, s2, k.w, lane4));
 }
 
-// MAC = false: the keystream only (out = in ^ S_1..; ccm_ctr_kernel), no
-// tag and no T-table rounds (lane4 unused).
-template <int NR, bool OPEN, int TAG, bool MAC = true>
+template <int NR, bool OPEN, int TAG>
 __device__ __forceinline__ void ccm_bs_record(const tg_batch& b, uint64_t i, bool valid, uint32_t lane4,
                                               const RkLds& rk, const bs8::KeyPlanesVmemFolded& km,
                                               uint32_t rows) {
@@ -510,13 +505,11 @@ __device__ __forceinline__ void ccm_bs_record(const tg_batch& b, uint64_t i, boo
     bs8::lane_consts<0>(1u, lanec, kmask);                // block j of a batch: counter 8 beta + 1 + j
 
     // E(S_0) masks the tag; B_0 and the AAD blocks start the MAC (aesccm.py:40-67)
-    uint4 s0 = make_uint4(0, 0, 0, 0), x = make_uint4(0, 0, 0, 0);
-    if constexpr (MAC) {
-        s0 = aes_block<NR>(lane4, rk, make_uint4(a0, a1, a2, a3));
-        if (valid)
-            ccm_mac_head<TAG>([&](uint4 blk) { x = aes_block<NR>(lane4, rk, xor_blk(x, blk)); }, nv, a1, a2, a3,
-                              len, ad, alen);
-    }
+    const uint4 s0 = aes_block<NR>(lane4, rk, make_uint4(a0, a1, a2, a3));
+    uint4 x = make_uint4(0, 0, 0, 0);
+    if (valid)
+        ccm_mac_head<TAG>([&](uint4 blk) { x = aes_block<NR>(lane4, rk, xor_blk(x, blk)); }, nv, a1, a2, a3,
+                          len, ad, alen);
     const uint32_t nfull = len >> 4, tail = len & 15, nblk = (len + 15) >> 4;
     uint32_t nb = (nblk + 7) >> 3;
 #pragma unroll
@@ -574,10 +567,10 @@ __device__ __forceinline__ void ccm_bs_record(const tg_batch& b, uint64_t i, boo
                 store_partial(out + 16u * blk, c, tail);
                 m = OPEN ? c : dd;
             }
-            if (MAC && blk < nblk) x = aes_block_rolled<NR>(lane4, rk, xor_blk(x, m));
+            if (blk < nblk) x = aes_block_rolled<NR>(lane4, rk, xor_blk(x, m));
         }
     }
-    if (!valid || !MAC) return;
+    if (!valid) return;
     const uint4 t = xor4(x, s0);   // the auth value; CCM_8 keeps its first 8 bytes
     if (!OPEN) {
         if (TAG == 16) {
@@ -670,184 +663,6 @@ int launch_hy(const AesKeyDev* key, const tg_batch& b, hipStream_t s) {
     return rc;
 }
 
-// ---- split: bitsliced keystream kernel || T-table CBC-MAC kernel ---------
-// The two AES streams of CCM on two kernels that run at the same time on
-// two internal streams: ccm_ctr_kernel (bitsliced, VALU; out = in ^ S_1..,
-// lane per record, ccm_bs_record<MAC = false>) and ccm_mac_kernel (T-table,
-// LDS; x = E(x ^ m) over the plaintext, then the tag or its check).  Each
-// kernel's waves get their own register allocation, so the MAC kernel's
-// light waves keep the LDS pipe fed while the keystream waves fill the VALU
-// -- which one kernel with both roles could not (its VGPR budget is the
-// larger role's, and the serial MAC chains then lack waves).  Seal: the MAC
-// reads the plaintext input, so the kernels are independent.  Open: the MAC
-// reads the plaintext the keystream kernel wrote, so the batch runs in
-// chunks, MAC(c) after CTR(c) and beside CTR(c + 1).
-template <int NR, bool OPEN, int TAG, int G>
-__device__ __forceinline__ void ccm_mac_record(const tg_batch& b, uint64_t i, uint32_t lane4,
-                                               const RkRegs<NR>& rk) {
-    const uint8_t* in = rec_in(b, i);
-    uint8_t* out = rec_out(b, i);
-    const uint32_t len = rec_len(b, i);
-    const uint8_t* ad = rec_aad(b, i);
-    const uint32_t alen = rec_aad_len(b, i);
-    const bool aligned = (((uintptr_t)in | (uintptr_t)out) & 15) == 0;
-    const uint4 nv = load_partial(b.nonce + 12 * i, 12);
-    const uint32_t a0 = 2u | (nv.x << 8);
-    const uint32_t a1 = (nv.x >> 24) | (nv.y << 8);
-    const uint32_t a2 = (nv.y >> 24) | (nv.z << 8);
-    const uint32_t a3 = nv.z >> 24;
-    const uint4 s0 = aes_block<NR>(lane4, rk, make_uint4(a0, a1, a2, a3));   // E(S_0)
-    uint4 x = make_uint4(0, 0, 0, 0);
-    ccm_mac_head<TAG>([&](uint4 blk) { x = aes_block<NR>(lane4, rk, xor_blk(x, blk)); }, nv, a1, a2, a3, len,
-                      ad, alen);
-    // the plaintext: seal's input, open's output (the keystream kernel's)
-    const uint8_t* m = OPEN ? out : in;
-    const uint32_t nfull = len >> 4, tail = len & 15;
-    uint32_t j = 0;
-    if (nfull >= (uint32_t)G) {
-        uint4 d[G];
-#pragma unroll
-        for (int q = 0; q < G; ++q) d[q] = load16(m + 16 * q, aligned);
-        for (; j + 2 * G <= nfull; j += G) {
-            uint4 nx[G];
-#pragma unroll
-            for (int q = 0; q < G; ++q) nx[q] = load16(m + 16 * (j + G + q), aligned);
-#pragma unroll
-            for (int q = 0; q < G; ++q) x = aes_block<NR>(lane4, rk, xor_blk(x, d[q]));
-#pragma unroll
-            for (int q = 0; q < G; ++q) d[q] = nx[q];
-        }
-#pragma unroll
-        for (int q = 0; q < G; ++q) x = aes_block<NR>(lane4, rk, xor_blk(x, d[q]));
-        j += G;
-    }
-    for (; j < nfull; ++j) x = aes_block<NR>(lane4, rk, xor_blk(x, load16(m + 16 * j, aligned)));
-    if (tail) x = aes_block<NR>(lane4, rk, xor_blk(x, load_partial(m + 16 * nfull, tail)));
-    const uint4 t = xor4(x, s0);
-    if (!OPEN) {
-        if (TAG == 16) {
-            store16(out + len, t, aligned && tail == 0);
-        } else {
-            store_partial(out + len, t, 8);
-        }
-        return;
-    }
-    const uint4 exp = TAG == 16 ? load16(in + len, aligned && tail == 0) : load_partial(in + len, 8);
-    uint32_t diff = (exp.x ^ t.x) | (exp.y ^ t.y);
-    if (TAG == 16) diff |= (exp.z ^ t.z) | (exp.w ^ t.w);
-    if (b.status) b.status[i] = diff == 0;
-    if (diff) {   // the keystream kernel already released this plaintext: zero it
-        const uint4 z = make_uint4(0, 0, 0, 0);
-        for (uint32_t k = 0; k < nfull; ++k) store16(out + 16 * k, z, aligned);
-        if (tail) store_partial(out + 16 * nfull, z, tail);
-    }
-}
-
-constexpr int kCcmCtrThreads = 256;
-constexpr uint32_t kCcmCtrRk = (kCcmCtrThreads / 64) * kCcmHyRowArea;   // rows areas, then round keys
-constexpr size_t kCcmCtrLds = kCcmCtrRk + 240;
-constexpr int kCcmMacG = 4;
-
-template <int NR>
-__global__ __launch_bounds__(kCcmCtrThreads) void ccm_ctr_kernel(const AesKeyDev* __restrict__ key, tg_batch b,
-                                                                 uint64_t first, uint64_t end,
-                                                                 const uint4* __restrict__ krows) {
-    if (threadIdx.x < 4 * (NR + 1))
-        reinterpret_cast<uint32_t*>(g_lds_ccm)[kCcmCtrRk / 4 + threadIdx.x] = key->rk[threadIdx.x];
-    __syncthreads();
-    const uint64_t i = first + (uint64_t)blockIdx.x * kCcmCtrThreads + threadIdx.x;
-    const uint32_t wave = threadIdx.x >> 6;
-    // every lane of the wave stays in (wave-wide batch count, shuffles)
-    ccm_bs_record<NR, false, 16, false>(b, i, i < end, 0u, RkLds{kCcmCtrRk}, bs8::KeyPlanesVmemFolded{{krows}},
-                                        wave * kCcmHyRowArea);
-}
-
-template <int NR, bool OPEN, int TAG>
-__global__ __launch_bounds__(1024) void ccm_mac_kernel(const AesKeyDev* __restrict__ key, tg_batch b,
-                                                       uint64_t first, uint64_t end) {
-    stage_te(reinterpret_cast<uint32_t*>(g_lds_ccm));
-    RkRegs<NR> rk;
-#pragma unroll
-    for (int k = 0; k < 4 * (NR + 1); ++k) rk.w[k] = key->rk[k];
-    __syncthreads();
-    const uint64_t i = first + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= end) return;
-    ccm_mac_record<NR, OPEN, TAG, kCcmMacG>(b, i, (threadIdx.x & 31u) << 2, rk);
-}
-
-// The split launch's two internal streams per device (created once, kept).
-struct SplitStreams {
-    hipStream_t ctr = nullptr, mac = nullptr;
-};
-int split_streams(SplitStreams& out) {
-    static std::mutex mu;
-    static SplitStreams per_dev[64];
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return TG_EHIP;
-    std::lock_guard<std::mutex> g(mu);
-    SplitStreams& s = per_dev[dev];
-    if (!s.ctr && hipStreamCreateWithFlags(&s.ctr, hipStreamNonBlocking) != hipSuccess) return TG_EHIP;
-    if (!s.mac && hipStreamCreateWithFlags(&s.mac, hipStreamNonBlocking) != hipSuccess) return TG_EHIP;
-    out = s;
-    return TG_OK;
-}
-
-// Open: records in chunks of this many (the MAC of chunk c waits for the
-// keystream of chunk c only).
-constexpr uint64_t kCcmSplitChunk = 1u << 17;
-
-template <int NR, bool OPEN, int TAG>
-int launch_split(const AesKeyDev* key, const tg_batch& b, hipStream_t s) {
-    if (lds_attr((const void*)ccm_ctr_kernel<NR>, (int)kCcmCtrLds)) return TG_EHIP;
-    if (lds_attr((const void*)ccm_mac_kernel<NR, OPEN, TAG>, (int)kCcmLds)) return TG_EHIP;
-    SplitStreams ss;
-    if (split_streams(ss)) return TG_EHIP;
-    uint32_t* scratch = nullptr;
-    if (stream_alloc((void**)&scratch, kCcmHyScratch, s)) return TG_EHIP;
-    hipLaunchKernelGGL(ccm_hy_setup_kernel, dim3(1), dim3(256), 0, s, key, NR, b, scratch);
-    const uint4* krows = reinterpret_cast<const uint4*>(scratch + 128);
-    std::vector<hipEvent_t> ev;
-    auto event = [&](hipStream_t st) -> hipEvent_t {
-        hipEvent_t e = nullptr;
-        if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return nullptr;
-        ev.push_back(e);
-        if (hipEventRecord(e, st) != hipSuccess) return nullptr;
-        return e;
-    };
-    int rc = hipGetLastError() == hipSuccess ? TG_OK : TG_EHIP;
-    hipEvent_t e0 = rc ? nullptr : event(s);
-    if (!e0) rc = TG_EHIP;
-    if (!rc && (hipStreamWaitEvent(ss.ctr, e0, 0) != hipSuccess || hipStreamWaitEvent(ss.mac, e0, 0) != hipSuccess))
-        rc = TG_EHIP;
-    const uint64_t chunk = OPEN ? kCcmSplitChunk : b.n;
-    for (uint64_t lo = 0; !rc && lo < b.n; lo += chunk) {
-        const uint64_t hi = b.n - lo < chunk ? b.n : lo + chunk;
-        hipLaunchKernelGGL((ccm_ctr_kernel<NR>), dim3((unsigned)((hi - lo + kCcmCtrThreads - 1) / kCcmCtrThreads)),
-                           dim3(kCcmCtrThreads), kCcmCtrLds, ss.ctr, key, b, lo, hi, krows);
-        if (hipGetLastError() != hipSuccess) {
-            rc = TG_EHIP;
-            break;
-        }
-        if (OPEN) {   // this chunk's MAC reads the plaintext the keystream kernel wrote
-            hipEvent_t ec = event(ss.ctr);
-            if (!ec || hipStreamWaitEvent(ss.mac, ec, 0) != hipSuccess) {
-                rc = TG_EHIP;
-                break;
-            }
-        }
-        hipLaunchKernelGGL((ccm_mac_kernel<NR, OPEN, TAG>), dim3((unsigned)((hi - lo + 1023) / 1024)), dim3(1024),
-                           kCcmLds, ss.mac, key, b, lo, hi);
-        if (hipGetLastError() != hipSuccess) rc = TG_EHIP;
-    }
-    // the caller's stream continues after both kernels
-    hipEvent_t ea = rc ? nullptr : event(ss.ctr), eb = rc ? nullptr : event(ss.mac);
-    if (!rc && (!ea || !eb || hipStreamWaitEvent(s, ea, 0) != hipSuccess || hipStreamWaitEvent(s, eb, 0) != hipSuccess))
-        rc = TG_EHIP;
-    if (stream_free(scratch, s) && !rc) rc = TG_EHIP;
-    for (hipEvent_t e : ev) (void)hipEventDestroy(e);   // released once complete
-    return rc;
-}
-
 template <int NR, bool OPEN, int TAG, bool TABLE>
 int launch_wave(const AesKeyDev* keys, uint64_t nkeys, const tg_batch& b, hipStream_t s) {
     if (lds_attr((const void*)ccm_wave_kernel<NR, OPEN, TAG, TABLE>, (int)kCcmWaveLds)) return TG_EHIP;
@@ -877,8 +692,7 @@ int launch_w(const AesKeyDev* keys, uint64_t nkeys, const tg_batch& b, hipStream
 // to kCcmWaveMaxRecords, else lane per record with the window cache), 1 =
 // lane per record, full rounds, 2 = wave per record, 3 = lane per record
 // with the window cache, 4 = the hybrid lane-per-record kernel (single key),
-// 5 / 6 / 7 / 8 = 3 with the payload loaded 1 / 2 / 4 / 8 blocks ahead, 9 =
-// the split keystream || MAC kernels (single key).
+// 5 / 6 / 7 / 8 = 3 with the payload loaded 1 / 2 / 4 / 8 blocks ahead.
 template <int NR, bool OPEN, int TAG, bool TABLE>
 int launch(const AesKeyDev* keys, uint64_t nkeys, const tg_batch& b, hipStream_t s) {
     switch (opt(kOptCcmVariant)) {
@@ -900,9 +714,7 @@ int launch(const AesKeyDev* keys, uint64_t nkeys, const tg_batch& b, hipStream_t
         case 6: return launch_w<NR, OPEN, TAG, TABLE, true, 2>(keys, nkeys, b, s);
         case 7: return launch_w<NR, OPEN, TAG, TABLE, true, 4>(keys, nkeys, b, s);
         case 8: return launch_w<NR, OPEN, TAG, TABLE, true, 8>(keys, nkeys, b, s);
-        case 9:
-            if (TABLE) return launch_w<NR, OPEN, TAG, TABLE, true>(keys, nkeys, b, s);
-            return launch_split<NR, OPEN, TAG>(keys, b, s);
+
         default: return TG_EINVAL;
     }
 }
