@@ -79,7 +79,11 @@ int tg_init(int device);                   /* hipSetDevice for the calling threa
  *   chacha_variant     0 auto, 3 wave per record, 4 lane per record with
  *                      the register-staged tile, 5 lane per record with the
  *                      LDS-DMA tile (auto's choice for large batches)
- *   ccm_variant        0 auto, 1 lane full rounds, 2 wave, 3 lane
+ *   ccm_variant        0 auto, 1 lane full rounds, 2 wave, 3 lane, 4 hybrid
+ *                      (bitsliced keystream + T-table MAC waves, single key),
+ *                      5 / 6 / 7 / 8 lane with the payload 1 / 2 / 4 / 8
+ *                      blocks ahead (auto's single-key choice: 4)
+ *   ccm_hy_t           T-table waves of the CCM hybrid (0 = 4 of 12, -1 none)
  *   waves_per_record   0 auto, 1 / 4 / 16
  *   no_plan            1 = no length-sorted launch order
  *   stage_copy         1 = per-record calls copy through device memory

@@ -38,8 +38,6 @@ LENS = [0, 1, 15, 16, 17, 63, 64, 65, 1000, 1024, 1040, 4095, 16383, 16384, 1638
     ("aesgcm", 32, {"gcm_variant": 15, "hy_threads": 768}),
     ("aesgcm", 16, {"gcm_variant": 15, "hy_t": 8, "hy_prio": 1}),   # round 2's split
     ("aesgcm", 16, {"gcm_variant": 15, "hy_t": 16}),   # T-table waves only
-    ("aesgcm", 16, {"gcm_variant": 15, "bs_touch": 1}),   # bitsliced waves touch the payload lines
-    ("aesgcm", 32, {"gcm_variant": 15, "bs_touch": -1}),
     ("aesgcm", 32, {"gcm_variant": 15, "hy_t": -1}),   # bitsliced waves only
     ("chacha", 32, {"chacha_variant": 4}),        # lane per record, register-staged tile fill
     ("chacha", 32, {"chacha_variant": 5}),        # lane per record, LDS-DMA tile fill (auto)
@@ -209,17 +207,16 @@ def test_key_table_octet_kernel(torch, tg, oracle_mod, klen, keys, align, varian
 
 @pytest.mark.parametrize("klen", [16, 32])
 @pytest.mark.parametrize("keys", [3, 300])
-@pytest.mark.parametrize("split,hyb,kt_t,touch", [(0, 0, 0, 0), (1000, 0, 0, 0), (0, 0, 1, 0), (1000, 0, 11, 0),
-                                                  (1000, -1, 0, 0), (0, 0, 0, 1), (0, 0, 0, -1)])
-def test_key_table_hybrid_kernel(torch, tg, oracle_mod, klen, keys, split, hyb, kt_t, touch):
+@pytest.mark.parametrize("split,hyb,kt_t", [(0, 0, 0), (1000, 0, 0), (0, 0, 1), (1000, 0, 11),
+                                            (1000, -1, 0)])
+def test_key_table_hybrid_kernel(torch, tg, oracle_mod, klen, keys, split, hyb, kt_t):
     """The key-table long records at 32 lanes per record on the persistent
     T-table + bitsliced kernel (aes_gcm_bs8.hip gcm_kth_kernel; kt_hybrid 0,
     the default): T-table waves at 32 lanes per record with per-half counter
     windows, bitsliced waves as in the key-grouped kernel, per-wave 4-bit
     GHASH tables rebuilt when a wave's key changes; kt_t 1 / 11 puts one / all
     waves on the T-table cipher; kt_hybrid -1 the bitsliced key-grouped
-    kernel; bs_touch 1 / -1 with and without the bitsliced waves' line
-    touches.  Ragged lengths around the batch and window boundaries, AES-128
+    kernel.  Ragged lengths around the batch and window boundaries, AES-128
     and AES-256, oracle-exact with tampered tags."""
     from batchpack import HostBatch, run_seal_open
     rng = np.random.default_rng(900 + klen + keys + split + kt_t + hyb)
@@ -229,7 +226,7 @@ def test_key_table_hybrid_kernel(torch, tg, oracle_mod, klen, keys, split, hyb, 
     kb = [rng.bytes(klen) for _ in range(keys)]
     obj = tg.KeyTable("aesgcm", kb)
     karr = np.frombuffer(b"".join(kb), np.uint8).reshape(keys, klen)
-    with tg.options(gcm_table_variant=0, kt_split=split, kt_lpr=32, kt_hybrid=hyb, kt_t=kt_t, bs_touch=touch):
+    with tg.options(gcm_table_variant=0, kt_split=split, kt_lpr=32, kt_hybrid=hyb, kt_t=kt_t):
         run_seal_open(torch, tg, oracle_mod, hb, "aesgcm", karr, obj, tamper=(4, 100, len(lens) - 1))
 
 

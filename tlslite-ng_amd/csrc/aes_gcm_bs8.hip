@@ -40,11 +40,9 @@ namespace tg {
 namespace {
 
 // Per-wave LDS of octet_job: the first-state planes of each record (128 B per
-// record slot, up to 8) at recw, round 1's S-box output of their rows 0 and 1
-// (64 B per slot) at recw + 1024, and at recw + 1536 the 256-byte landing
-// area of the bitsliced role's line touches (octet_job ``touch``).
-constexpr uint32_t kRecArea = 1792;
-constexpr uint32_t kTouchOff = 1536;
+// record slot, up to 8) at recw, and round 1's S-box output of their rows 0
+// and 1 (64 B per slot) at recw + 1024.
+constexpr uint32_t kRecArea = 1536;
 
 constexpr int kBs8Threads = 512;
 constexpr int kBs8Recs = kBs8Threads / 8;               // record slots per workgroup
@@ -205,18 +203,12 @@ struct TableKeyCtx {    // a key of a key table: the wave's 4-bit H^8 tables in 
 // kc.gmul multiplies by H^LPR), batch beta of the lane holds its blocks
 // rho + LPR (8 beta + j), j = 0..7, so each load / store instruction still
 // moves LPR x 16 consecutive bytes per record (whole 128-byte lines).
-// touch (bitsliced role): the wave-uniform LDS address of a 256-byte area,
-// or 0.  Before a batch's cipher runs, one 4-byte LDS-DMA load per block of
-// the batch (global_load_lds_dword, no VGPR) brings the payload's lines into
-// the caches, so the loads after the cipher hit L2 instead of waiting on HBM
-// -- the payload itself held in VGPRs across the cipher spills (PRE).  The
-// landed bytes are never read.
 template <int NR, bool OPEN, bool TROLE, class KM, class KC, bool PRE = false, int LPR = 8,
           class RKT = RkLds>
 __device__ __forceinline__ void octet_job(const KC& kc, const tg_batch& b,
                                           const uint32_t* __restrict__ order, uint64_t t0,
                                           uint32_t recw, const RKT& rkT, uint32_t sbox,
-                                          const KM& km, uint32_t touch = 0) {
+                                          const KM& km) {
     static_assert(LPR == 8 || LPR == 16 || LPR == 32 || LPR == 64, "lanes per record");
     static_assert(LPR == 8 || LPR == 32 || !TROLE, "the T-table role runs octets or pairs");
     constexpr uint32_t kM = LPR - 1, kS = LPR == 8 ? 3 : LPR == 16 ? 4 : LPR == 32 ? 5 : 6;
@@ -437,15 +429,7 @@ __device__ __forceinline__ void octet_job(const KC& kc, const tg_batch& b,
 #pragma unroll
                 for (int q = 0; q < 8; ++q) dp[q] = gload16u(in + 16u * (blk0 + LPR * q));
             }
-#if defined(__HIP_DEVICE_COMPILE__)
-            if (!PRE && touch && valid && blk0 < (nfast << (kS + 3))) {
-#pragma unroll
-                for (int q = 0; q < 8; ++q)
-                    __builtin_amdgcn_global_load_lds(
-                        (const __attribute__((address_space(1))) void*)(in + 16u * (blk0 + LPR * q)),
-                        (__attribute__((address_space(3))) void*)(uintptr_t)touch, 4, 0, 0);
-            }
-#endif
+
             uint32_t w[4][8];
             bs8::encrypt<NR>(s, km, w, hi);
             uint4 ks[8];
@@ -557,7 +541,7 @@ __global__ __launch_bounds__(THREADS) void gcm_hy_kernel(const GcmKeyDev* __rest
                                                             uint32_t nt, uint32_t prio,
                                                             const uint4* __restrict__ krows,
                                                             const uint4* __restrict__ rkrot,
-                                                            const uint4* __restrict__ masks, uint32_t touch) {
+                                                            const uint4* __restrict__ masks) {
     stage_ghash_rot(g_lds_bs8, key->ghash8, kHyJt);
     stage_te(reinterpret_cast<uint32_t*>(g_lds_bs8) + kTeBase / 4);
     stage_sbox(kHySbox);
@@ -595,7 +579,7 @@ __global__ __launch_bounds__(THREADS) void gcm_hy_kernel(const GcmKeyDev* __rest
             const tg_batch b = *bp;
             octet_job<NR, OPEN, false, bs8::KeyPlanesVmemFolded, SingleKeyRowCtx, (THREADS < 1024)>(
                 SingleKeyRowCtx{key, jw, masks}, b, order, 8ull * job, recw, none, kHySbox,
-                bs8::KeyPlanesVmemFolded{{krows}}, touch ? recw + kTouchOff : 0u);
+                bs8::KeyPlanesVmemFolded{{krows}});
         }
     }
 }
@@ -665,13 +649,12 @@ int launch_hy_kernels(const GcmKeyDev* key, const tg_batch& b, hipStream_t s, co
     }
     const uint4* krows = reinterpret_cast<const uint4*>(key->bs8rows);
     const uint4* rkrot = reinterpret_cast<const uint4*>(key->rkrot);
-    const uint32_t touch = opt(kOptBsTouch) > 0 ? 1u : 0u;   // option bs_touch (0 = off here)
     if (small)
         hipLaunchKernelGGL((gcm_hy_kernel<NR, OPEN, 768>), dim3((unsigned)device_cus()), dim3(768), kHyLds, s,
-                           key, (const tg_batch*)bcopy, order, queue, nt, prio, krows, rkrot, masks, touch);
+                           key, (const tg_batch*)bcopy, order, queue, nt, prio, krows, rkrot, masks);
     else
         hipLaunchKernelGGL((gcm_hy_kernel<NR, OPEN, 1024>), dim3((unsigned)device_cus()), dim3(1024), kHyLds,
-                           s, key, (const tg_batch*)bcopy, order, queue, nt, prio, krows, rkrot, masks, touch);
+                           s, key, (const tg_batch*)bcopy, order, queue, nt, prio, krows, rkrot, masks);
     return hipGetLastError() == hipSuccess ? TG_OK : TG_EHIP;
 }
 
@@ -793,8 +776,7 @@ constexpr int kKthWaves = 11;
 constexpr int kKthThreads = kKthWaves * 64;
 constexpr uint32_t kKthSbox = 2 * 65536 + 3 * 8192;
 constexpr uint32_t kKthRec = kKthSbox + 256;
-constexpr uint32_t kKthRecArea = 640;                   // (64 / 32) x 128 + (64 / 32) x 64, touch area
-constexpr uint32_t kKthTouchOff = 384;
+constexpr uint32_t kKthRecArea = 384;                   // (64 / 32) x 128 + (64 / 32) x 64
 constexpr size_t kKthLds = kKthRec + kKthWaves * kKthRecArea;
 constexpr uint32_t kKthChunk = 2;   // jobs per grab (1 / 2 / 4 / 8: 607 / 614 / 610 / 590 GiB/s, profiles/r04/r4j)
 constexpr int kKthTDefault = 7;
@@ -815,8 +797,7 @@ __global__ __launch_bounds__(kKthThreads) void gcm_kth_kernel(const GcmTableKey*
                                                              const uint32_t* __restrict__ nlong_p,
                                                              const uint4* __restrict__ masks,
                                                              const uint32_t* __restrict__ jobkey,
-                                                             uint32_t* __restrict__ queue, uint32_t nt,
-                                                             uint32_t touch) {
+                                                             uint32_t* __restrict__ queue, uint32_t nt) {
     stage_te(reinterpret_cast<uint32_t*>(g_lds_bs8) + kTeBase / 4);
     stage_sbox(kKthSbox);
     __syncthreads();
@@ -866,7 +847,7 @@ __global__ __launch_bounds__(kKthThreads) void gcm_kth_kernel(const GcmTableKey*
                     kc, bj, order, p0, recw, RkTab{keys[k].rk, rot + 16u * k}, kKthSbox, km);
             else
                 octet_job<NR, OPEN, false, bs8::KeyPlanesVmemFolded, TableKeyCtx, false, 32>(
-                    kc, bj, order, p0, recw, RkLds{0}, kKthSbox, km, touch ? recw + kKthTouchOff : 0u);
+                    kc, bj, order, p0, recw, RkLds{0}, kKthSbox, km);
         }
         if (tail) break;
     }
@@ -984,8 +965,7 @@ int launch_kth(const GcmTableKey* keys, const uint4* hpow, const uint32_t* plane
     hipLaunchKernelGGL(kth_jobkey_kernel, dim3((unsigned)((b.n + 256) / 256)), dim3(256), 0, s, jobpos, njobs,
                        nlong, order, b.key_idx, jobkey);
     hipLaunchKernelGGL((gcm_kth_kernel<NR, OPEN>), dim3((unsigned)device_cus()), dim3(kKthThreads), kKthLds, s,
-                       keys, hpow, planes, rot, b, order, jobpos, njobs, nlong, masks, jobkey, queue, nt,
-                       opt(kOptBsTouch) > 0 ? 1u : 0u);
+                       keys, hpow, planes, rot, b, order, jobpos, njobs, nlong, masks, jobkey, queue, nt);
     return hipGetLastError() == hipSuccess ? TG_OK : TG_EHIP;
 }
 

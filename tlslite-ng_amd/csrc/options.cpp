@@ -30,7 +30,6 @@ constexpr OptName kNames[kOptCount] = {
     {"kt_hybrid", "TLSGPU_KT_HYBRID"},
     {"kt_t", "TLSGPU_KT_T"},
     {"ccm_hy_t", "TLSGPU_CCM_HY_T"},
-    {"bs_touch", "TLSGPU_BS_TOUCH"},
 };
 
 std::atomic<int> g_val[kOptCount];

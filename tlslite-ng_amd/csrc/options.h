@@ -28,8 +28,6 @@ enum Opt {
     kOptKtT,                  // TLSGPU_KT_T: T-table waves of that kernel (0 = auto)
     kOptCcmHyT,               // TLSGPU_CCM_HY_T: T-table waves of the AES-CCM hybrid kernel
                               // (0 = auto, -1 none)
-    kOptBsTouch,              // TLSGPU_BS_TOUCH: bitsliced AES-GCM waves touch a batch's
-                              // payload lines before the cipher (1 on, -1 off, 0 auto)
     kOptCount
 };
 
