@@ -15,6 +15,8 @@
 #                  -> kernel_stats.csv
 #   pmc            tools/pmc_full.sh passes of the headline kernels
 #   traffic        tools/traffic.sh FETCH_SIZE / WRITE_SIZE passes -> traffic.json
+#   c4fetch        FETCH_SIZE / WRITE_SIZE passes over one config-4 seal + open
+#                  -> c4fetch<suffix>.txt (per-dispatch sums by kernel)
 #   ab=LIBA,LIBB   alternate two built libraries (tools/gpu_lib_ab.sh) -> ab.txt
 # A step may carry its own environment after '@' (comma-separated, e.g.
 # ccm@TLSGPU_CCM_VARIANT=4,TLSGPU_CCM_HY_T=-1); its output file then takes the
@@ -71,6 +73,14 @@ for st0 in "$@"; do
       python3 tools/pmc_summary.py $O > $O/fetch$SUF.txt 2>&1 || true; head -40 $O/fetch$SUF.txt ;;
     traffic)
       bash tools/traffic.sh $T ;;
+    c4fetch)
+      for c in FETCH_SIZE WRITE_SIZE; do
+        (cd /tmp && export TMPDIR=/tmp && timeout -k 10 240 rocprofv3 --pmc $c --kernel-trace --output-format csv \
+          -d $O/c4fetch$SUF/p_$c -o pass -- python3 $R/bench.py --config c4 --steps 1 --warmup 0 --no-cpu-baseline \
+          > $O/c4fetch_$c$SUF.log 2>&1)
+      done
+      PROF_RECORDS=1 PROF_LEN=6103244480 python3 tools/pmc_summary.py $O/c4fetch$SUF > $O/c4fetch$SUF.txt 2>&1 || true
+      grep -E "==|FETCH|WRITE" $O/c4fetch$SUF.txt | head -40 ;;
     ab=*)
       L=${st#ab=}; bash tools/gpu_lib_ab.sh $T ${L%,*} ${L#*,} ;;
     *) echo "unknown step $st"; exit 2 ;;

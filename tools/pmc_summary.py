@@ -14,7 +14,7 @@ from collections import defaultdict
 
 def short(name):
     import re
-    m = re.search(r"(gcm_kernel<[^>]*>|gcm_hy_kernel<[^>]*>|gcm_kth_kernel<[^>]*>|gcm_table_vkernel<[^>]*>|gcm_bs8?_kernel<[^>]*>|chacha_kernel<[^>]*>|chacha_wave_kernel<[^>]*>|ccm_\w*kernel<[^>]*>|k_copy_\w+)", name)
+    m = re.search(r"(gcm_kernel<[^>]*>|gcm_hy_kernel<[^>]*>|gcm_kth_kernel<[^>]*>|gcm_table_vkernel<[^>]*>|gcm_bs8?_kernel<[^>]*>|chacha_kernel<[^>]*>|chacha_wave_kernel<[^>]*>|ccm_\w*kernel<[^>]*>|kt_mask_kernel<[^>]*>|kth_jobkey_kernel|k_copy_\w+)", name)
     return m.group(1) if m else None
 
 
