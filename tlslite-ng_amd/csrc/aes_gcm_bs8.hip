@@ -213,6 +213,12 @@ __device__ __forceinline__ void octet_job(const KC& kc, const tg_batch& b,
     static_assert(LPR == 8 || LPR == 32 || !TROLE, "the T-table role runs octets or pairs");
     constexpr uint32_t kM = LPR - 1, kS = LPR == 8 ? 3 : LPR == 16 ? 4 : LPR == 32 ? 5 : 6;
     const uint32_t* rk = kc.rk();
+    // payload loads and stores with the non-temporal hint: read or written
+    // once, they no longer push the tables, key rows and per-key material out
+    // of L2 (single key: AES-128-GCM seal / open -1.6 / -1.3 %,
+    // profiles/r05/r5l/; key table: config 4 +1.5 %, FETCH_SIZE -4 to -6 %,
+    // r5k/)
+    constexpr bool kNt = true;
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t l = lane & kM;
     const uint64_t t = t0 + (lane >> kS);
@@ -300,13 +306,18 @@ __device__ __forceinline__ void octet_job(const KC& kc, const tg_batch& b,
                 uint4 d[N];
 #pragma unroll
                 for (int q = 0; q < N; ++q)
-                    d[q] = pre ? pre[q] : gload16u(in + 16u * (blk0 + LPR * (j0 + q)));
+                    d[q] = pre ? pre[q]
+                               : kNt ? gload16u_nt(in + 16u * (blk0 + LPR * (j0 + q)))
+                                     : gload16u(in + 16u * (blk0 + LPR * (j0 + q)));
 #pragma unroll
                 for (int q = 0; q < N; ++q) {
                     const uint4 k = ks[q];
                     const uint4 c = make_uint4(xor3(d[q].x, k.x, rkl.x), xor3(d[q].y, k.y, rkl.y),
                                                xor3(d[q].z, k.z, rkl.z), xor3(d[q].w, k.w, rkl.w));
-                    gstore16u(out + 16u * (blk0 + LPR * (j0 + q)), c);
+                    if constexpr (kNt)
+                        gstore16u_nt(out + 16u * (blk0 + LPR * (j0 + q)), c);
+                    else
+                        gstore16u(out + 16u * (blk0 + LPR * (j0 + q)), c);
                     if (!OPEN) d[q] = c;
                 }
 #pragma unroll
@@ -381,7 +392,9 @@ __device__ __forceinline__ void octet_job(const KC& kc, const tg_batch& b,
                 const bool fast = blk0 < (nfast << (kS + 3));
                 if (fast && valid) {
 #pragma unroll
-                    for (int q = 0; q < 4; ++q) dp[q] = gload16u(in + 16u * (blk0 + LPR * (4 * h + q)));
+                    for (int q = 0; q < 4; ++q)
+                        dp[q] = kNt ? gload16u_nt(in + 16u * (blk0 + LPR * (4 * h + q)))
+                                    : gload16u(in + 16u * (blk0 + LPR * (4 * h + q)));
                 }
                 if constexpr (LPR == 8) {
                     t_half<NR>(lane4, rkT, cc, c0, win, wc, k0w, h, ks);
@@ -427,7 +440,8 @@ __device__ __forceinline__ void octet_job(const KC& kc, const tg_batch& b,
             const bool pre = PRE && blk0 < (nfast << (kS + 3));
             if (pre && valid) {
 #pragma unroll
-                for (int q = 0; q < 8; ++q) dp[q] = gload16u(in + 16u * (blk0 + LPR * q));
+                for (int q = 0; q < 8; ++q)
+                    dp[q] = kNt ? gload16u_nt(in + 16u * (blk0 + LPR * q)) : gload16u(in + 16u * (blk0 + LPR * q));
             }
 
             uint32_t w[4][8];

@@ -132,7 +132,11 @@ __device__ __forceinline__ void gstore16(uint8_t* p, uint4 v) {
 typedef u32x4 u32x4_u1 __attribute__((aligned(1)));
 __device__ __forceinline__ uint4 gload16u(const uint8_t* p) {
 #if defined(__HIP_DEVICE_COMPILE__)
+#if defined(TG_NT_IO)
+    const u32x4 v = __builtin_nontemporal_load((const __attribute__((address_space(1))) u32x4_u1*)p);
+#else
     const u32x4 v = *(const __attribute__((address_space(1))) u32x4_u1*)p;
+#endif
     return make_uint4(v.x, v.y, v.z, v.w);
 #else
     return uint4();
@@ -140,7 +144,29 @@ __device__ __forceinline__ uint4 gload16u(const uint8_t* p) {
 }
 __device__ __forceinline__ void gstore16u(uint8_t* p, uint4 v) {
 #if defined(__HIP_DEVICE_COMPILE__)
+#if defined(TG_NT_IO)
+    __builtin_nontemporal_store(u32x4{v.x, v.y, v.z, v.w}, (__attribute__((address_space(1))) u32x4_u1*)p);
+#else
     *(__attribute__((address_space(1))) u32x4_u1*)p = u32x4{v.x, v.y, v.z, v.w};
+#endif
+#endif
+}
+
+// gload16u / gstore16u with the non-temporal hint: payload that is read or
+// written once and should not push other data out of L2 (aes_gcm_bs8.hip
+// octet_job: the key material and GHASH rows it re-reads every batch stay
+// resident).
+__device__ __forceinline__ uint4 gload16u_nt(const uint8_t* p) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    const u32x4 v = __builtin_nontemporal_load((const __attribute__((address_space(1))) u32x4_u1*)p);
+    return make_uint4(v.x, v.y, v.z, v.w);
+#else
+    return uint4();
+#endif
+}
+__device__ __forceinline__ void gstore16u_nt(uint8_t* p, uint4 v) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    __builtin_nontemporal_store(u32x4{v.x, v.y, v.z, v.w}, (__attribute__((address_space(1))) u32x4_u1*)p);
 #endif
 }
 

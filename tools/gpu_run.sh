@@ -8,6 +8,7 @@
 #   bench          bench.py (headline, CPU baseline)   -> bench.json
 #   bench-nocpu    bench.py --no-cpu-baseline          -> bench.json
 #   c4 | c5 | ccm | c1 | e2e | ingest                  -> bench_<step>.json
+#   distself       bench.py --dist-selftest: RCCL at world size 1 -> bench_dist_selftest.json
 #   n2             bench.py --gpus 2 --config c5 --records 65536 over gloo on
 #                  one MI355X (both ranks on the one device), CPU baseline on
 #                  -> bench_n2_c5.json; and the headline leg -> bench_n2.json
@@ -51,6 +52,9 @@ for st0 in "$@"; do
     c4|c5|ccm|c1|ingest)
       timeout -k 10 600 python -u bench.py --config $st $BENCH_ARGS > $O/bench_$st$SUF.json 2> $O/bench_$st$SUF.err
       cat $O/bench_$st$SUF.json ;;
+    distself)
+      timeout -k 10 600 python -u bench.py --dist-selftest --no-cpu-baseline $BENCH_ARGS > $O/bench_dist_selftest.json 2> $O/bench_dist_selftest.err
+      cat $O/bench_dist_selftest.json ;;
     e2e)
       timeout -k 10 600 python -u bench.py --e2e --no-cpu-baseline $BENCH_ARGS > $O/bench_e2e.json 2> $O/bench_e2e.err; cat $O/bench_e2e.json ;;
     n2)
