@@ -547,6 +547,30 @@ static_assert(kTeBase == 65536, "Te block follows the GHASH tables");
 // faster than the plain planes and 3 % faster than LDS-staged ones, whose
 // LDS reads compete with the T-table waves; profiles/r02/v58_fold_keys/,
 // v25_hy_keys.txt).
+#if defined(TG_TAIL_PROBE)   // measurement build: the persistent loop's end spread
+__device__ unsigned long long g_tp[8] = {~0ull, 0, ~0ull, 0, 0, 0, 0, 0};
+__device__ __forceinline__ void tail_probe_start() {
+    if ((threadIdx.x & 63u) == 0) atomicMin(&g_tp[0], (unsigned long long)__builtin_amdgcn_s_memrealtime());
+}
+__device__ __forceinline__ void tail_probe_end(bool trole) {
+    if ((threadIdx.x & 63u) == 0) {
+        const unsigned long long t = __builtin_amdgcn_s_memrealtime();
+        atomicMax(&g_tp[1], t);
+        atomicMin(&g_tp[2], t);
+        atomicAdd(&g_tp[3], t - g_tp[0]);
+        atomicAdd(&g_tp[4], 1ull);
+        atomicMax(&g_tp[trole ? 5 : 6], t);
+    }
+}
+__global__ void tail_probe_print() {
+    const unsigned long long t0 = g_tp[0];
+    printf("TAIL_PROBE kernel_us %.1f first_end_us %.1f mean_end_us %.1f last_T_us %.1f last_bs_us %.1f waves %llu\n",
+           (g_tp[1] - t0) / 100.0, (g_tp[2] - t0) / 100.0, g_tp[3] / (100.0 * g_tp[4]), (g_tp[5] - t0) / 100.0,
+           (g_tp[6] - t0) / 100.0, g_tp[4]);
+    g_tp[0] = ~0ull; g_tp[1] = 0; g_tp[2] = ~0ull; g_tp[3] = 0; g_tp[4] = 0; g_tp[5] = 0; g_tp[6] = 0;
+}
+#endif
+
 template <int NR, bool OPEN, int THREADS>
 __global__ __launch_bounds__(THREADS) void gcm_hy_kernel(const GcmKeyDev* __restrict__ key,
                                                             const tg_batch* bp,
@@ -562,6 +586,9 @@ __global__ __launch_bounds__(THREADS) void gcm_hy_kernel(const GcmKeyDev* __rest
     if (threadIdx.x < 4 * (NR + 1)) reinterpret_cast<uint32_t*>(g_lds_bs8)[kHyRk / 4 + threadIdx.x] = key->rk[threadIdx.x];
     __syncthreads();
     const uint32_t wave = (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+#if defined(TG_TAIL_PROBE)
+    tail_probe_start();
+#endif
     const uint64_t njobs = (bp->n + 7) / 8;
     const uint32_t recw = kHyRecBase + wave * kRecArea;
     const uint4 jw = lds_u128(kHyJt + ((threadIdx.x & 15u) << 4));
@@ -596,6 +623,9 @@ __global__ __launch_bounds__(THREADS) void gcm_hy_kernel(const GcmKeyDev* __rest
                 bs8::KeyPlanesVmemFolded{{krows}});
         }
     }
+#if defined(TG_TAIL_PROBE)
+    tail_probe_end(wave < nt);
+#endif
 }
 
 // Stream-ordered setup of the hybrid kernel's scratch: the job counter and a
@@ -669,6 +699,9 @@ int launch_hy_kernels(const GcmKeyDev* key, const tg_batch& b, hipStream_t s, co
     else
         hipLaunchKernelGGL((gcm_hy_kernel<NR, OPEN, 1024>), dim3((unsigned)device_cus()), dim3(1024), kHyLds,
                            s, key, (const tg_batch*)bcopy, order, queue, nt, prio, krows, rkrot, masks);
+#if defined(TG_TAIL_PROBE)
+    hipLaunchKernelGGL(tail_probe_print, dim3(1), dim3(1), 0, s);
+#endif
     return hipGetLastError() == hipSuccess ? TG_OK : TG_EHIP;
 }
 
