@@ -222,6 +222,10 @@ __device__ __forceinline__ void octet_job(const KC& kc, const tg_batch& b,
     // the bitsliced role's short last batches on a T-table half (key-table
     // hybrid: its bitsliced waves get the job key's rotated copy too)
     constexpr bool kShortT = !TROLE && LPR == 32 && std::is_same<RKT, RkTab>::value;
+#if !defined(TG_KT_SHORT_MAX)
+#define TG_KT_SHORT_MAX 5   // A/B builds: 7 / 8 measured 0.5 % slower (profiles/r05/r5v/)
+#endif
+    constexpr uint32_t kShortMax = TG_KT_SHORT_MAX;
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t l = lane & kM;
     const uint64_t t = t0 + (lane >> kS);
@@ -416,20 +420,26 @@ __device__ __forceinline__ void octet_job(const KC& kc, const tg_batch& b,
             const uint4 nvr = valid ? load_partial(b.nonce + 12 * i, 12) : make_uint4(0, 0, 0, 0);
             uint4 ks[1] = {xor4(aes_block_sb<NR>(rk, make_uint4(nvr.x, nvr.y, nvr.z, bswap32(c0)), sbox), rkl)};
             consume(ks, blk0, 0, std::integral_constant<int, 1>(), nullptr);
-        } else if (kShortT && __all(!valid || nvl <= 8u * beta + 4u)) {
-            // bitsliced role, a record's last batch with at most four blocks
-            // per lane: one T-table half (the T-table role's code, its Te
-            // copies and rotated key) instead of eight bitsliced blocks; the
-            // keystream is final, so the bitsliced last-round-key term that
-            // consume() adds is added here once more to cancel it
+        } else if (kShortT && __all(!valid || nvl < 8u * beta + kShortMax)) {
+            // bitsliced role, a record's last batch with fewer than
+            // kShortMax blocks per lane: T-table halves (the T-table role's
+            // code, its Te copies and rotated key) instead of eight bitsliced
+            // blocks; the keystream is final, so the bitsliced
+            // last-round-key term that consume() adds is added here once more
+            // to cancel it
             const CtrCache cct = ctr_cache<NR>(lane4, rkT, nv);
-            const bool winh = __all(((c0 ^ (c0 + 3u * LPR)) >> 8) == 0);
-            const uint4 wch = winh ? win_consts<NR>(lane4, rkT, cct, c0) : make_uint4(0, 0, 0, 0);
-            uint4 ks[4];
-            t_half<NR, LPR>(lane4, rkT, cct, c0, winh, wch, rkT.get(0).w, 0, ks);
+#pragma unroll 1
+            for (int h = 0; h < 2; ++h) {
+                if (h == 1 && __all(!valid || nvl <= 8u * beta + 4u)) break;
+                const uint32_t ch = c0 + 4u * LPR * h;
+                const bool winh = __all(((ch ^ (ch + 3u * LPR)) >> 8) == 0);
+                const uint4 wch = winh ? win_consts<NR>(lane4, rkT, cct, ch) : make_uint4(0, 0, 0, 0);
+                uint4 ks[4];
+                t_half<NR, LPR>(lane4, rkT, cct, c0, winh, wch, rkT.get(0).w, h, ks);
 #pragma unroll
-            for (int q = 0; q < 4; ++q) ks[q] = xor4(ks[q], rkl);
-            consume(ks, blk0, 0, std::integral_constant<int, 4>(), nullptr);
+                for (int q = 0; q < 4; ++q) ks[q] = xor4(ks[q], rkl);
+                consume(ks, blk0, 4 * h, std::integral_constant<int, 4>(), nullptr);
+            }
         } else {
             // counters of this batch below 2^16 (wave-uniform): rows 0-1
             // come in after round 1's SubBytes (bs8::encrypt sub01)
