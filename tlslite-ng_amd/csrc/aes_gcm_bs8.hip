@@ -852,7 +852,18 @@ constexpr uint32_t kKthSbox = 2 * 65536 + 3 * 8192;
 constexpr uint32_t kKthRec = kKthSbox + 256;
 constexpr uint32_t kKthRecArea = 384;                   // (64 / 32) x 128 + (64 / 32) x 64
 constexpr size_t kKthLds = kKthRec + kKthWaves * kKthRecArea;
-constexpr uint32_t kKthChunk = 2;   // jobs per grab (1 / 2 / 4 / 8: 607 / 614 / 610 / 590 GiB/s, profiles/r04/r4j)
+// A planned job holds up to kKthGroup pairs of one key (the plan's job size
+// is 2 kKthGroup records): its waves run them pair by pair with one table
+// build.  kKthChunk planned jobs per grab.
+#if !defined(TG_KTH_GROUP)
+// 2: two pairs of one key per grab, one table build; against two planned
+// pairs per grab (1): 666.6-668.0 vs 663.6-665.0 GiB/s, 4: 657.7-659.9
+// (three rounds, profiles/r05/r5x/)
+#define TG_KTH_GROUP 2
+#endif
+constexpr uint32_t kKthGroup = TG_KTH_GROUP;
+// jobs per grab (1 / 2 / 4 / 8: 607 / 614 / 610 / 590 GiB/s, profiles/r04/r4j)
+constexpr uint32_t kKthChunk = kKthGroup == 1 ? 2 : 1;
 constexpr int kKthTDefault = 7;
 static_assert(kKthLds <= 163840, "key-table hybrid LDS");
 
@@ -891,8 +902,8 @@ __global__ __launch_bounds__(kKthThreads) void gcm_kth_kernel(const GcmTableKey*
         // (chunk of two: the values by selects, so the loop body -- both
         // roles' code -- exists once)
         const uint32_t pa = gld(jobpos, j0), pb = gld(jobpos, j0 + 1u),
-                       pc = j0 + 2u <= njobs ? gld(jobpos, j0 + 2u) : 0u;
-        const uint32_t ka = gld(jobkey, j0), kb = j0 + 1u < njobs ? gld(jobkey, j0 + 1u) : 0u;
+                       pc = kKthChunk > 1 && j0 + 2u <= njobs ? gld(jobpos, j0 + 2u) : 0u;
+        const uint32_t ka = gld(jobkey, j0), kb = kKthChunk > 1 && j0 + 1u < njobs ? gld(jobkey, j0 + 1u) : 0u;
         bool tail = false;
         for (uint32_t q = 0; q < j1 - j0; ++q) {
             const uint32_t p0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)(q ? pb : pa));
@@ -912,16 +923,18 @@ __global__ __launch_bounds__(kKthThreads) void gcm_kth_kernel(const GcmTableKey*
                 cur = k;
                 __builtin_amdgcn_wave_barrier();
             }
-            tg_batch bj = b;
-            bj.n = p1;   // the job's slots are p0 .. p1 - 1 (at most two)
             const TableKeyCtx kc{keys[k].rk, hpow + 64u * k, tab, masks};
             const bs8::KeyPlanesVmemFolded km{{reinterpret_cast<const uint4*>(planes + kKtPlaneWords * k)}};
-            if (wave < nt)
-                octet_job<NR, OPEN, true, bs8::KeyPlanesVmemFolded, TableKeyCtx, false, 32, RkTab>(
-                    kc, bj, order, p0, recw, RkTab{keys[k].rk, rot + 16u * k}, kKthSbox, km);
-            else
-                octet_job<NR, OPEN, false, bs8::KeyPlanesVmemFolded, TableKeyCtx, false, 32, RkTab>(
-                    kc, bj, order, p0, recw, RkTab{keys[k].rk, rot + 16u * k}, kKthSbox, km);
+            for (uint32_t pp = p0; pp < p1; pp += 2u) {   // the planned job's pairs
+                tg_batch bj = b;
+                bj.n = pp + 2u < p1 ? pp + 2u : p1;   // the pair's slots are pp .. bj.n - 1
+                if (wave < nt)
+                    octet_job<NR, OPEN, true, bs8::KeyPlanesVmemFolded, TableKeyCtx, false, 32, RkTab>(
+                        kc, bj, order, pp, recw, RkTab{keys[k].rk, rot + 16u * k}, kKthSbox, km);
+                else
+                    octet_job<NR, OPEN, false, bs8::KeyPlanesVmemFolded, TableKeyCtx, false, 32, RkTab>(
+                        kc, bj, order, pp, recw, RkTab{keys[k].rk, rot + 16u * k}, kKthSbox, km);
+            }
         }
         if (tail) break;
     }
@@ -1075,7 +1088,8 @@ int launch_kt(const GcmTableKey* keys, uint64_t nkeys, const uint4* hpow, const 
     if (b.n == 0) return TG_OK;
     if (b.n > 0xfffffffeull || !b.key_idx) return TG_EINVAL;
     if (lpr != 0 && lpr != 8 && lpr != 16 && lpr != 32 && lpr != 64) return TG_EINVAL;
-    const uint32_t jobsz = lpr ? 64u / (uint32_t)lpr : 1u;
+    // the key-table hybrid plans groups of kKthGroup pairs (gcm_kth_kernel)
+    const uint32_t jobsz = lpr ? (64u / (uint32_t)lpr) * (lpr == 32 && hybrid ? kKthGroup : 1u) : 1u;
     size_t plan = 0;
     int rc = tg_key_job_plan(b.key_idx, b.len, b.fixed_len, b.n, nkeys, split, jobsz, nullptr, nullptr,
                              nullptr, nullptr, nullptr, &plan, s);
