@@ -837,11 +837,11 @@ __global__ __launch_bounds__(kKtThreads, 4) void gcm_kt_kernel(const GcmTableKey
 // persistent workgroup of 11 waves per CU; waves 0 .. nt - 1 run the T-table
 // cipher (Te0/Te2 copies at kTeBase, the job key's round keys by scalar
 // loads, its rotated copy from the per-key ``rot`` table), the rest the
-// bitsliced one (the key's folded plane rows).  A job is up to two records of
-// one key (tg_key_job_plan, 32 lanes per record), a wave takes kKthChunk
-// consecutive jobs at a time -- the plan orders jobs by key, so consecutive
-// jobs mostly share their key -- and rebuilds its 4-bit GHASH tables of the
-// key's H^32 (8 KiB, build_table4) only when the key changes.  LDS (160 KiB):
+// bitsliced one (the key's folded plane rows).  A planned job is up to
+// kKthGroup pairs of records of one key (tg_key_job_plan, 32 lanes per
+// record, a pair per octet_job); a wave takes kKthChunk planned jobs at a
+// time and rebuilds its 4-bit GHASH tables of the key's H^32 (8 KiB,
+// build_table4) only when the key changes.  LDS (160 KiB):
 // eight waves' tables below the Te block, three above it, the S-box and a
 // 384-byte record area per wave (two records' first-state planes and their
 // round-1 rows).  11 waves: the Te block and 11 tables fill the LDS (3 waves
