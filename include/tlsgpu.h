@@ -76,6 +76,9 @@ int tg_init(int device);                   /* hipSetDevice for the calling threa
  *                      the persistent T-table + bitsliced kernel, -1 = the
  *                      bitsliced key-grouped kernel; its T-table waves (0 =
  *                      7 of 11, at most 11)
+ *   kt_overlap         key tables: the short records' lane kernel on the
+ *                      engine's second stream beside the long records'
+ *                      kernel (0 = on, -1 = both on the caller's stream)
  *   chacha_variant     0 auto, 3 wave per record, 4 lane per record with
  *                      the register-staged tile, 5 lane per record with the
  *                      LDS-DMA tile (auto's choice for large batches)

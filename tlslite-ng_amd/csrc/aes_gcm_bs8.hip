@@ -1082,6 +1082,26 @@ int launch_kt_jobs(const GcmTableKey* keys, uint64_t nkeys, const uint4* hpow, c
 // (aes_gcm.hip gcm_table_vkernel) over the tail of the same plan, which the
 // planner leaves sorted by length, longest first.  split 0: every in-range
 // record takes the long kernel; split ~0u: every record the lane kernel.
+// The key-table launches' second stream, one per device, created on first
+// use at the lowest priority: the short records' lane kernel runs there
+// beside the long records' kernel, so the CUs the long kernel's tail leaves
+// idle take lane-kernel workgroups instead of waiting for the whole grid.
+hipStream_t kt_aux_stream() {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return nullptr;
+    static std::mutex m;
+    static std::map<int, hipStream_t> streams;
+    std::lock_guard<std::mutex> g(m);
+    auto it = streams.find(dev);
+    if (it != streams.end()) return it->second;
+    int lo = 0, hi = 0;
+    if (hipDeviceGetStreamPriorityRange(&lo, &hi) != hipSuccess) lo = 0;
+    hipStream_t x = nullptr;
+    if (hipStreamCreateWithPriority(&x, hipStreamNonBlocking, lo) != hipSuccess) return nullptr;
+    streams[dev] = x;
+    return x;
+}
+
 template <int NR, bool OPEN>
 int launch_kt(const GcmTableKey* keys, uint64_t nkeys, const uint4* hpow, const uint32_t* planes,
               const uint4* rot, const tg_batch& b, hipStream_t s, uint32_t split, int lpr, bool hybrid) {
@@ -1106,6 +1126,17 @@ int launch_kt(const GcmTableKey* keys, uint64_t nkeys, const uint4* hpow, const 
     uint32_t* nlong = njobs + 1;
     rc = tg_key_job_plan(b.key_idx, b.len, b.fixed_len, b.n, nkeys, split, jobsz, order, jobpos, njobs, nlong,
                          buf + so + sj + 256, &plan, s);
+    // the lane kernel's records (plan slots [nlong, n)) are disjoint from the
+    // long kernel's: it runs on the second stream, forked after the plan and
+    // joined before the scratch goes back (option kt_overlap -1: one stream)
+    hipStream_t s2 = nullptr;
+    hipEvent_t fork = nullptr, join = nullptr;
+    if (!rc && split != 0xffffffffu && opt(kOptKtOverlap) >= 0 && (s2 = kt_aux_stream()) != nullptr) {
+        if (hipEventCreateWithFlags(&fork, hipEventDisableTiming) != hipSuccess ||
+            hipEventCreateWithFlags(&join, hipEventDisableTiming) != hipSuccess ||
+            hipEventRecord(fork, s) != hipSuccess || hipStreamWaitEvent(s2, fork, 0) != hipSuccess)
+            rc = TG_EHIP;
+    }
     if (!rc && split != 0xffffffffu) {
         switch (lpr) {
             case 0:   // the long records one per wavefront (plan slots [0, nlong))
@@ -1123,7 +1154,13 @@ int launch_kt(const GcmTableKey* keys, uint64_t nkeys, const uint4* hpow, const 
             default: rc = launch_kt_jobs<NR, OPEN, 64>(keys, nkeys, hpow, planes, b, s, order, jobpos, njobs, nlong); break;
         }
     }
-    if (!rc) rc = tg_launch_gcm_table_lane(keys, nkeys, NR, b, OPEN, s, order, nlong);
+    if (!rc) rc = tg_launch_gcm_table_lane(keys, nkeys, NR, b, OPEN, s2 && join ? s2 : s, order, nlong);
+    if (s2 && join) {   // rejoin (also after a failed launch: the scratch must outlive both streams' work)
+        if ((hipEventRecord(join, s2) != hipSuccess || hipStreamWaitEvent(s, join, 0) != hipSuccess) && !rc)
+            rc = TG_EHIP;
+    }
+    if (fork) (void)hipEventDestroy(fork);
+    if (join) (void)hipEventDestroy(join);
     if (stream_free(buf, s)) return TG_EHIP;
     return rc;
 }

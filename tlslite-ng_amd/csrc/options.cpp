@@ -29,6 +29,7 @@ constexpr OptName kNames[kOptCount] = {
     {"hy_threads", "TLSGPU_HY_THREADS"},
     {"kt_hybrid", "TLSGPU_KT_HYBRID"},
     {"kt_t", "TLSGPU_KT_T"},
+    {"kt_overlap", "TLSGPU_KT_OVERLAP"},
     {"ccm_hy_t", "TLSGPU_CCM_HY_T"},
 };
 

@@ -26,6 +26,8 @@ enum Opt {
     kOptKtHybrid,             // TLSGPU_KT_HYBRID: key-table long records on the T-table +
                               // bitsliced persistent kernel (1) or the bitsliced one (-1), 0 auto
     kOptKtT,                  // TLSGPU_KT_T: T-table waves of that kernel (0 = auto)
+    kOptKtOverlap,            // TLSGPU_KT_OVERLAP: key-table lane kernel on a second stream beside
+                              // the long records' kernel (0 = auto, on; -1 = one stream)
     kOptCcmHyT,               // TLSGPU_CCM_HY_T: T-table waves of the AES-CCM hybrid kernel
                               // (0 = auto, -1 none)
     kOptCount
