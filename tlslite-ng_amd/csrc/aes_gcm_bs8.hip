@@ -1086,9 +1086,12 @@ int launch_kt_jobs(const GcmTableKey* keys, uint64_t nkeys, const uint4* hpow, c
 // use at the lowest priority: the short records' lane kernel runs there
 // beside the long records' kernel, so the CUs the long kernel's tail leaves
 // idle take lane-kernel workgroups instead of waiting for the whole grid.
-hipStream_t kt_aux_stream() {
+hipStream_t kt_aux_stream(hipStream_t s) {
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess) return nullptr;
+    // the caller's stream on another device than the current one: no overlap
+    hipDevice_t sd = 0;
+    if (hipStreamGetDevice(s, &sd) == hipSuccess && (int)sd != dev) return nullptr;
     static std::mutex m;
     static std::map<int, hipStream_t> streams;
     std::lock_guard<std::mutex> g(m);
@@ -1131,7 +1134,7 @@ int launch_kt(const GcmTableKey* keys, uint64_t nkeys, const uint4* hpow, const 
     // joined before the scratch goes back (option kt_overlap -1: one stream)
     hipStream_t s2 = nullptr;
     hipEvent_t fork = nullptr, join = nullptr;
-    if (!rc && split != 0xffffffffu && opt(kOptKtOverlap) >= 0 && (s2 = kt_aux_stream()) != nullptr) {
+    if (!rc && split != 0xffffffffu && opt(kOptKtOverlap) >= 0 && (s2 = kt_aux_stream(s)) != nullptr) {
         if (hipEventCreateWithFlags(&fork, hipEventDisableTiming) != hipSuccess ||
             hipEventCreateWithFlags(&join, hipEventDisableTiming) != hipSuccess ||
             hipEventRecord(fork, s) != hipSuccess || hipStreamWaitEvent(s2, fork, 0) != hipSuccess)
