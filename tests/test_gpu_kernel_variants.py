@@ -207,17 +207,19 @@ def test_key_table_octet_kernel(torch, tg, oracle_mod, klen, keys, align, varian
 
 @pytest.mark.parametrize("klen", [16, 32])
 @pytest.mark.parametrize("keys", [3, 300])
-@pytest.mark.parametrize("split,hyb,kt_t", [(0, 0, 0), (1000, 0, 0), (0, 0, 1), (1000, 0, 11),
-                                            (1000, -1, 0)])
-def test_key_table_hybrid_kernel(torch, tg, oracle_mod, klen, keys, split, hyb, kt_t):
+@pytest.mark.parametrize("split,hyb,kt_t,ovl", [(0, 0, 0, 0), (1000, 0, 0, 0), (0, 0, 1, 0), (1000, 0, 11, 0),
+                                                (1000, -1, 0, 0), (1000, 0, 0, -1)])
+def test_key_table_hybrid_kernel(torch, tg, oracle_mod, klen, keys, split, hyb, kt_t, ovl):
     """The key-table long records at 32 lanes per record on the persistent
     T-table + bitsliced kernel (aes_gcm_bs8.hip gcm_kth_kernel; kt_hybrid 0,
     the default): T-table waves at 32 lanes per record with per-half counter
     windows, bitsliced waves as in the key-grouped kernel, per-wave 4-bit
     GHASH tables rebuilt when a wave's key changes; kt_t 1 / 11 puts one / all
     waves on the T-table cipher; kt_hybrid -1 the bitsliced key-grouped
-    kernel.  Ragged lengths around the batch and window boundaries, AES-128
-    and AES-256, oracle-exact with tampered tags."""
+    kernel; kt_overlap -1 keeps the short records' lane kernel on the
+    caller's stream instead of the engine's second stream.  Ragged lengths
+    around the batch and window boundaries, AES-128 and AES-256, oracle-exact
+    with tampered tags."""
     from batchpack import HostBatch, run_seal_open
     rng = np.random.default_rng(900 + klen + keys + split + kt_t + hyb)
     lens = LENS * 3 + list(rng.integers(0, 16401, 500)) + [2047, 2048, 2049, 4095, 4096, 4097, 4111,
@@ -226,7 +228,7 @@ def test_key_table_hybrid_kernel(torch, tg, oracle_mod, klen, keys, split, hyb, 
     kb = [rng.bytes(klen) for _ in range(keys)]
     obj = tg.KeyTable("aesgcm", kb)
     karr = np.frombuffer(b"".join(kb), np.uint8).reshape(keys, klen)
-    with tg.options(gcm_table_variant=0, kt_split=split, kt_lpr=32, kt_hybrid=hyb, kt_t=kt_t):
+    with tg.options(gcm_table_variant=0, kt_split=split, kt_lpr=32, kt_hybrid=hyb, kt_t=kt_t, kt_overlap=ovl):
         run_seal_open(torch, tg, oracle_mod, hb, "aesgcm", karr, obj, tamper=(4, 100, len(lens) - 1))
 
 
