@@ -76,9 +76,10 @@ int tg_init(int device);                   /* hipSetDevice for the calling threa
  *                      the persistent T-table + bitsliced kernel, -1 = the
  *                      bitsliced key-grouped kernel; its T-table waves (0 =
  *                      7 of 11, at most 11)
- *   kt_overlap         key tables: the short records' lane kernel on the
- *                      engine's second stream beside the long records'
- *                      kernel (0 = on, -1 = both on the caller's stream)
+ *   kt_overlap         key tables: the short records' lane kernel on a
+ *                      helper stream of the caller's stream beside the long
+ *                      records' kernel (0 = on, -1 = both on the caller's
+ *                      stream)
  *   chacha_variant     0 auto, 3 wave per record, 4 lane per record with
  *                      the register-staged tile, 5 lane per record with the
  *                      LDS-DMA tile (auto's choice for large batches)
@@ -296,8 +297,21 @@ int tg_selftest_ghash(int mode, const uint8_t* h, const uint8_t* aad, const uint
 
 /* Diagnostics: the per-launch scratch the library holds (the buffers of
  * its scratch cache, all devices) -- bounded by the launches in flight, not
- * by the streams a caller has used.  Test and monitoring use. */
+ * by the streams a caller has used.  Test and monitoring use.
+ * A batch call borrows a scratch buffer and gives it back behind its work
+ * on the caller's stream; the next call on the same stream handle may take
+ * it again at once, and that call's stream then waits for the buffer's
+ * last work, so a stream destroyed with work pending and a new stream that
+ * receives its handle stay correct.
+ * tg_scratch_trim: frees cached scratch buffers whose work has completed
+ *   until at most keep_bytes remain, and every idle helper stream (the
+ *   second stream a key-table batch runs its short records on).  The cache
+ *   also trims itself before it grows past 8 GiB.
+ * tg_helper_info: helper streams the library holds, and how many a batch
+ *   is using right now (one per caller stream in flight, at most). */
 int tg_scratch_info(uint64_t* bytes, uint64_t* buffers);
+int tg_scratch_trim(uint64_t keep_bytes);
+int tg_helper_info(uint64_t* streams, uint64_t* busy);
 
 /* Device memory helpers so a ctypes host needs no other GPU runtime. */
 int tg_malloc(void** p, size_t bytes);

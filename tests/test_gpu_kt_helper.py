@@ -1,0 +1,174 @@
+"""GPU: key-table batches on independent streams stay independent (ADVICE
+r05).
+
+A key-table AES-GCM batch of mixed lengths runs its long records on the
+key-table hybrid kernel and its short ones (< 2 048 B) on the lane kernel,
+which goes to a helper stream forked from the caller's stream
+(aes_gcm_bs8.hip launch_kt, api.hip helper_fork / helper_join).  Round 5 had
+ONE helper per device: a second caller's short records queued behind the
+first caller's, so the second caller's stream waited for the first one's.
+Here:
+
+* a caller whose stream is held up (a spin kernel ahead of its batch) does
+  not hold up another caller's batch on another stream;
+* two threads, each with its own torch stream and key table, seal and open
+  config-4-shaped batches at once, and every record of both is compared with
+  the C oracle (tests/fullcheck.py) and opened back.
+
+Reference: one cipher state per connection direction, used independently
+(recordlayer.py:239-249; aesgcm.py:101-154 per record).
+"""
+import threading
+
+import numpy as np
+import pytest
+
+from vectors import tls13_aad
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def torch():
+    import torch as t
+    if not t.cuda.is_available():
+        pytest.fail("GPU tests need a visible MI355X")
+    return t
+
+
+@pytest.fixture(scope="module")
+def tg(torch):
+    import tlsgpu
+    return tlsgpu
+
+
+class KtJob(object):
+    """One config-4-shaped key-table batch: n records over nkeys AES-256 keys,
+    lengths mixed around the 2 048-byte split (so both kernels run), TLS 1.3
+    nonces and AADs computed on the host."""
+
+    def __init__(self, torch, tg, seed, n=12288, nkeys=700):
+        import fullcheck
+        rng = np.random.default_rng(seed)
+        self.n = n
+        self.keys = rng.integers(0, 256, (nkeys, 32), dtype=np.uint8)
+        short = rng.integers(0, 2048, n // 3)
+        long_ = rng.integers(2048, 16385, n - n // 3)
+        lens = np.concatenate([short, long_]).astype(np.int64)
+        rng.shuffle(lens)
+        lens[:4] = [16384, 0, 2047, 2048]
+        self.lens = lens
+        self.key_idx = rng.integers(0, nkeys, n).astype(np.uint32)
+        step = (lens + 15) // 16 * 16
+        self.in_off = np.concatenate([[0], np.cumsum(step)[:-1]]).astype(np.int64)
+        ostep = (lens + 16 + 15) // 16 * 16
+        self.out_off = np.concatenate([[0], np.cumsum(ostep)[:-1]]).astype(np.int64)
+        iv = rng.bytes(12)
+        self.nonces_h = fullcheck.tls13_nonces(iv, 77 * seed, n)
+        self.aad_h = np.frombuffer(b"".join(bytes(tls13_aad(int(L))) for L in lens), np.uint8).copy()
+        self.aad_off = np.arange(n, dtype=np.int64) * 5
+        g = torch.Generator(device="cuda").manual_seed(seed)
+        self.inp = torch.randint(0, 256, (int(step.sum()) + 16,), dtype=torch.uint8, device="cuda",
+                                 generator=g)
+        self.sealed = torch.zeros(int(ostep.sum()) + 16, dtype=torch.uint8, device="cuda")
+        self.back = torch.zeros_like(self.inp)
+        # the bytes that are record payload (records sit at 16-byte aligned offsets)
+        m = np.zeros(self.inp.numel(), bool)
+        for o, L in zip(self.in_off, lens):
+            m[o:o + L] = True
+        self.payload = torch.from_numpy(m).cuda()
+        self.status = torch.zeros(n, dtype=torch.uint8, device="cuda")
+        d = lambda a: torch.from_numpy(np.ascontiguousarray(a)).cuda()  # noqa: E731
+        self.d_lens = d(lens.astype(np.uint32).view(np.int32))
+        self.d_in_off, self.d_out_off = d(self.in_off), d(self.out_off)
+        self.d_nonces = d(self.nonces_h.reshape(-1))
+        self.d_aad, self.d_aad_off = d(self.aad_h), d(self.aad_off)
+        self.d_kidx = d(self.key_idx.view(np.int32))
+        self.table = tg.KeyTable("aesgcm", [bytes(k) for k in self.keys])
+
+    def seal(self, tg, stream):
+        tg.seal_batch(self.table, tg.make_batch(self.n, self.inp, self.sealed, self.d_nonces, aad=self.d_aad,
+                                                lens=self.d_lens, in_off=self.d_in_off, out_off=self.d_out_off,
+                                                aad_off=self.d_aad_off, fixed_aad_len=5,
+                                                key_idx=self.d_kidx), stream)
+
+    def open(self, tg, stream):
+        tg.open_batch(self.table, tg.make_batch(self.n, self.sealed, self.back, self.d_nonces, aad=self.d_aad,
+                                                lens=self.d_lens, in_off=self.d_out_off, out_off=self.d_in_off,
+                                                aad_off=self.d_aad_off, fixed_aad_len=5, key_idx=self.d_kidx,
+                                                status=self.status), stream)
+
+    def check(self, torch, oracle_mod):
+        import fullcheck
+        recs, _ = fullcheck.check_all(torch, oracle_mod, "aesgcm", self.keys, self.inp, self.in_off, self.lens,
+                                      self.sealed, self.out_off, self.nonces_h, self.aad_h, self.aad_off,
+                                      np.full(self.n, 5), key_idx=self.key_idx)
+        assert recs == self.n
+        assert bool((self.status == 1).all())
+        assert torch.equal(self.back[self.payload], self.inp[self.payload])
+
+
+def test_held_up_caller_does_not_hold_up_another(torch, tg, oracle_mod):
+    a = KtJob(torch, tg, 1)
+    b = KtJob(torch, tg, 2)
+    sa, sb = torch.cuda.Stream(), torch.cuda.Stream()
+    # warm both tables' first launches (plan scratch, helper creation)
+    a.seal(tg, sa)
+    b.seal(tg, sb)
+    torch.cuda.synchronize()
+    done_a = torch.cuda.Event()
+    with torch.cuda.stream(sa):
+        torch.cuda._sleep(400_000_000)   # ~0.2 s at 2 GHz: stream A is busy
+    a.seal(tg, sa)
+    done_a.record(sa)
+    b.seal(tg, sb)
+    sb.synchronize()
+    # B's batch (a few ms) finished while A still sleeps; with one shared
+    # helper stream B's short records would have queued behind A's
+    a_pending = not done_a.query()
+    torch.cuda.synchronize()
+    assert a_pending, "stream B waited for stream A's work"
+    streams, busy = tg.helper_info()
+    assert busy == 0 and streams >= 2, (streams, busy)
+    for j in (a, b):
+        j.open(tg, None)
+    torch.cuda.synchronize()
+    a.check(torch, oracle_mod)
+    b.check(torch, oracle_mod)
+
+
+def test_two_threads_key_tables_concurrent(torch, tg, oracle_mod):
+    jobs = [KtJob(torch, tg, 10 + t) for t in range(2)]
+    errors = []
+    barrier = threading.Barrier(2)
+
+    def run(j):
+        try:
+            st = torch.cuda.Stream()
+            with torch.cuda.stream(st):
+                barrier.wait()
+                for _ in range(3):
+                    j.seal(tg, st)
+                    j.open(tg, st)
+                st.synchronize()
+        except Exception as e:   # noqa: BLE001 -- reported below
+            errors.append(e)
+
+    threads = [threading.Thread(target=run, args=(j,)) for j in jobs]
+    for t in threads:
+        t.start()
+    for t in threads:
+        t.join(120)
+    assert not any(t.is_alive() for t in threads), "a key-table thread did not finish"
+    assert not errors, errors
+    torch.cuda.synchronize()
+    for j in jobs:
+        j.check(torch, oracle_mod)
+    assert tg.helper_info()[1] == 0
+    # trimming frees the idle helpers and scratch; the next batch makes them again
+    tg.scratch_trim(0)
+    assert tg.helper_info()[0] == 0
+    jobs[0].seal(tg, None)
+    jobs[0].open(tg, None)
+    torch.cuda.synchronize()
+    jobs[0].check(torch, oracle_mod)

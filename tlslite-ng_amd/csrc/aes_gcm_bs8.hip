@@ -1082,29 +1082,12 @@ int launch_kt_jobs(const GcmTableKey* keys, uint64_t nkeys, const uint4* hpow, c
 // (aes_gcm.hip gcm_table_vkernel) over the tail of the same plan, which the
 // planner leaves sorted by length, longest first.  split 0: every in-range
 // record takes the long kernel; split ~0u: every record the lane kernel.
-// The key-table launches' second stream, one per device, created on first
-// use at the lowest priority: the short records' lane kernel runs there
-// beside the long records' kernel, so the CUs the long kernel's tail leaves
-// idle take lane-kernel workgroups instead of waiting for the whole grid.
-hipStream_t kt_aux_stream(hipStream_t s) {
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess) return nullptr;
-    // the caller's stream on another device than the current one: no overlap
-    hipDevice_t sd = 0;
-    if (hipStreamGetDevice(s, &sd) == hipSuccess && (int)sd != dev) return nullptr;
-    static std::mutex m;
-    static std::map<int, hipStream_t> streams;
-    std::lock_guard<std::mutex> g(m);
-    auto it = streams.find(dev);
-    if (it != streams.end()) return it->second;
-    int lo = 0, hi = 0;
-    if (hipDeviceGetStreamPriorityRange(&lo, &hi) != hipSuccess) lo = 0;
-    hipStream_t x = nullptr;
-    if (hipStreamCreateWithPriority(&x, hipStreamNonBlocking, lo) != hipSuccess) return nullptr;
-    streams[dev] = x;
-    return x;
-}
-
+// The lane kernel runs on a helper stream of the caller's stream (api.hip
+// helper_fork / helper_join: idle or last used by this caller, so two
+// callers never chain through one helper), forked after the plan and joined
+// before the scratch goes back: the CUs the long kernel's tail leaves idle
+// take lane-kernel workgroups instead of waiting for the whole grid
+// (+0.4 %, profiles/r05/r5z/).  Option kt_overlap -1: one stream.
 template <int NR, bool OPEN>
 int launch_kt(const GcmTableKey* keys, uint64_t nkeys, const uint4* hpow, const uint32_t* planes,
               const uint4* rot, const tg_batch& b, hipStream_t s, uint32_t split, int lpr, bool hybrid) {
@@ -1130,16 +1113,10 @@ int launch_kt(const GcmTableKey* keys, uint64_t nkeys, const uint4* hpow, const 
     rc = tg_key_job_plan(b.key_idx, b.len, b.fixed_len, b.n, nkeys, split, jobsz, order, jobpos, njobs, nlong,
                          buf + so + sj + 256, &plan, s);
     // the lane kernel's records (plan slots [nlong, n)) are disjoint from the
-    // long kernel's: it runs on the second stream, forked after the plan and
+    // long kernel's: it runs on a helper stream, forked after the plan and
     // joined before the scratch goes back (option kt_overlap -1: one stream)
     hipStream_t s2 = nullptr;
-    hipEvent_t fork = nullptr, join = nullptr;
-    if (!rc && split != 0xffffffffu && opt(kOptKtOverlap) >= 0 && (s2 = kt_aux_stream(s)) != nullptr) {
-        if (hipEventCreateWithFlags(&fork, hipEventDisableTiming) != hipSuccess ||
-            hipEventCreateWithFlags(&join, hipEventDisableTiming) != hipSuccess ||
-            hipEventRecord(fork, s) != hipSuccess || hipStreamWaitEvent(s2, fork, 0) != hipSuccess)
-            rc = TG_EHIP;
-    }
+    if (!rc && split != 0xffffffffu && opt(kOptKtOverlap) >= 0) rc = helper_fork(s, &s2);
     if (!rc && split != 0xffffffffu) {
         switch (lpr) {
             case 0:   // the long records one per wavefront (plan slots [0, nlong))
@@ -1157,13 +1134,9 @@ int launch_kt(const GcmTableKey* keys, uint64_t nkeys, const uint4* hpow, const 
             default: rc = launch_kt_jobs<NR, OPEN, 64>(keys, nkeys, hpow, planes, b, s, order, jobpos, njobs, nlong); break;
         }
     }
-    if (!rc) rc = tg_launch_gcm_table_lane(keys, nkeys, NR, b, OPEN, s2 && join ? s2 : s, order, nlong);
-    if (s2 && join) {   // rejoin (also after a failed launch: the scratch must outlive both streams' work)
-        if ((hipEventRecord(join, s2) != hipSuccess || hipStreamWaitEvent(s, join, 0) != hipSuccess) && !rc)
-            rc = TG_EHIP;
-    }
-    if (fork) (void)hipEventDestroy(fork);
-    if (join) (void)hipEventDestroy(join);
+    if (!rc) rc = tg_launch_gcm_table_lane(keys, nkeys, NR, b, OPEN, s2 ? s2 : s, order, nlong);
+    // rejoin (also after a failed launch: the scratch must outlive both streams' work)
+    if (s2 && helper_join(s2, s) && !rc) rc = TG_EHIP;
     if (stream_free(buf, s)) return TG_EHIP;
     return rc;
 }

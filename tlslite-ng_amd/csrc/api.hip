@@ -539,13 +539,18 @@ int lds_attr(const void* fn, int bytes) {
 // Per-launch scratch (common.h stream_alloc / stream_free): a process-wide
 // list of device buffers, each free for reuse once the event recorded behind
 // its last launch has completed.  A buffer released on a stream is taken
-// again at once only by the next launch on that same stream (stream order
-// protects it) -- never through hipStreamPerThread or the null stream, whose
-// handle names a different stream in each thread.  So memory is bounded by
-// the launches in flight, not by the streams a caller has ever used, and
-// nothing is keyed on a stream handle.  (The device memory
-// pool of hipMallocAsync measured 4.7 MB more per stream used, without
-// reuse across streams: profiles/r05/r5b.)
+// again at once only by the next launch on that same stream handle -- never
+// through hipStreamPerThread or the null stream, whose handle names a
+// different stream in each thread -- and that launch's stream also waits for
+// the buffer's event, so a handle that a destroyed stream left behind and a
+// new stream took over cannot reuse a buffer whose work is still pending
+// (on the stream that recorded the event the wait orders
+// nothing new).  So memory is bounded by the launches in flight, not by the
+// streams a caller has ever used.  (The device memory pool of
+// hipMallocAsync measured 4.7 MB more per stream used, without reuse across
+// streams: profiles/r05/r5b.)  Idle buffers are freed by tg_scratch_trim,
+// and by stream_alloc itself once the cache holds more than kScratchHigh
+// bytes.
 namespace {
 struct ScratchBuf {
     void* p = nullptr;
@@ -561,6 +566,33 @@ std::vector<ScratchBuf>& scratch_list() {
     return *v;
 }
 bool per_thread_handle(hipStream_t s) { return s == nullptr || s == hipStreamPerThread; }
+constexpr size_t kScratchHigh = (size_t)8 << 30;
+
+// Frees idle buffers whose last launch has completed until the cache holds
+// at most ``keep`` bytes, largest first (g_scratch_mu held).  hipFree of an
+// idle buffer waits for nothing: its event has completed.
+void trim_locked(size_t keep) {
+    auto& v = scratch_list();
+    size_t total = 0;
+    for (const auto& b : v) total += b.cap;
+    while (total > keep) {
+        size_t best = v.size();
+        for (size_t i = 0; i < v.size(); ++i) {
+            const ScratchBuf& b = v[i];
+            if (b.busy || (b.done && hipEventQuery(b.done) != hipSuccess)) continue;
+            if (best == v.size() || b.cap > v[best].cap) best = i;
+        }
+        if (best == v.size()) return;   // everything left is in use
+        int cur = 0;
+        const bool switch_dev = hipGetDevice(&cur) == hipSuccess && cur != v[best].dev;
+        if (switch_dev) (void)hipSetDevice(v[best].dev);
+        (void)hipFree(v[best].p);
+        if (v[best].done) (void)hipEventDestroy(v[best].done);
+        if (switch_dev) (void)hipSetDevice(cur);
+        total -= v[best].cap;
+        v.erase(v.begin() + (std::ptrdiff_t)best);
+    }
+}
 }  // namespace
 
 int stream_alloc(void** p, size_t bytes, hipStream_t s) {
@@ -570,14 +602,22 @@ int stream_alloc(void** p, size_t bytes, hipStream_t s) {
     std::lock_guard<std::mutex> g(g_scratch_mu);
     auto& v = scratch_list();
     ScratchBuf* pick = nullptr;
+    bool pick_pending = false;
     for (auto& b : v) {
         if (b.busy || b.dev != dev || b.cap < bytes) continue;
+        const bool complete = !b.done || hipEventQuery(b.done) == hipSuccess;
         const bool ordered = b.last == s && !per_thread_handle(s);
-        if (ordered || !b.done || hipEventQuery(b.done) == hipSuccess) {
-            if (!pick || b.cap < pick->cap) pick = &b;
+        if (complete || ordered) {
+            if (!pick || b.cap < pick->cap) {
+                pick = &b;
+                pick_pending = !complete;
+            }
         }
     }
     if (!pick) {
+        size_t total = 0;
+        for (const auto& b : v) total += b.cap;
+        if (total + bytes > kScratchHigh) trim_locked(kScratchHigh > bytes ? kScratchHigh - bytes : 0);
         ScratchBuf nb;
         nb.cap = bytes < (1u << 20) ? (size_t)1 << 20 : (bytes + 0xfffff) & ~(size_t)0xfffff;
         nb.dev = dev;
@@ -588,6 +628,8 @@ int stream_alloc(void** p, size_t bytes, hipStream_t s) {
         }
         v.push_back(nb);
         pick = &v.back();
+    } else if (pick_pending && hipStreamWaitEvent(s, pick->done, 0) != hipSuccess) {
+        return TG_EHIP;
     }
     pick->busy = true;
     *p = pick->p;
@@ -601,15 +643,131 @@ void scratch_totals(uint64_t* bytes, uint64_t* buffers) {
     for (const auto& b : scratch_list()) *bytes += b.cap;
 }
 
+// The event is recorded first: only once the record has succeeded is the
+// buffer reusable.  If it fails the buffer stays busy (leaked, never handed
+// out behind a stale event) and the caller gets TG_EHIP.
 int stream_free(void* p, hipStream_t s) {
     std::lock_guard<std::mutex> g(g_scratch_mu);
     for (auto& b : scratch_list()) {
         if (b.p != p) continue;
+        if (hipEventRecord(b.done, s) != hipSuccess) return TG_EHIP;
         b.busy = false;
         b.last = s;
-        return hipEventRecord(b.done, s) == hipSuccess ? TG_OK : TG_EHIP;
+        return TG_OK;
     }
     return TG_EINVAL;
+}
+
+// Helper streams (common.h helper_fork / helper_join): a process-wide pool.
+// A launch that runs a second kernel beside its main one (the key-table
+// short records, aes_gcm_bs8.hip launch_kt) takes a helper of its device and
+// priority class that is idle -- its last join has completed -- or that
+// its own stream used last, so independent callers never queue behind each
+// other's helper work (round 5 had one helper per device shared
+// by every caller).  A caller at raised priority gets a helper at its own
+// priority; any other caller one at the lowest priority (the short records
+// fill the CUs the long kernel's tail leaves idle, profiles/r05/r5z/).
+namespace {
+struct HelperStream {
+    hipStream_t h = nullptr;
+    int dev = -1;
+    int prio = 0;
+    hipEvent_t fork = nullptr, join = nullptr;
+    hipStream_t last = nullptr;
+    bool busy = false;
+};
+std::mutex g_helper_mu;
+std::vector<HelperStream>& helper_list() {
+    static std::vector<HelperStream>* v = new std::vector<HelperStream>();
+    return *v;
+}
+}  // namespace
+
+int helper_fork(hipStream_t s, hipStream_t* out) {
+    *out = nullptr;
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return TG_EHIP;
+    // the caller's stream on another device than the current one: no helper
+    hipDevice_t sd = 0;
+    if (hipStreamGetDevice(s, &sd) == hipSuccess && (int)sd != dev) return TG_OK;
+    int least = 0, greatest = 0, sp = 0;
+    if (hipDeviceGetStreamPriorityRange(&least, &greatest) != hipSuccess) least = greatest = 0;
+    if (hipStreamGetPriority(s, &sp) != hipSuccess) sp = 0;
+    // priorities: lower numbers run first; 0 is the default
+    const int prio = sp < 0 && least != greatest ? sp : least;
+    std::lock_guard<std::mutex> g(g_helper_mu);
+    auto& v = helper_list();
+    HelperStream* pick = nullptr;
+    for (auto& x : v) {
+        if (x.busy || x.dev != dev || x.prio != prio) continue;
+        if ((x.last == s && !per_thread_handle(s)) || hipEventQuery(x.join) == hipSuccess) {
+            pick = &x;
+            break;
+        }
+    }
+    if (!pick) {
+        HelperStream x;
+        x.dev = dev;
+        x.prio = prio;
+        if (hipStreamCreateWithPriority(&x.h, hipStreamNonBlocking, prio) != hipSuccess) return TG_EHIP;
+        if (hipEventCreateWithFlags(&x.fork, hipEventDisableTiming) != hipSuccess ||
+            hipEventCreateWithFlags(&x.join, hipEventDisableTiming) != hipSuccess) {
+            if (x.fork) (void)hipEventDestroy(x.fork);
+            (void)hipStreamDestroy(x.h);
+            return TG_EHIP;
+        }
+        v.push_back(x);
+        pick = &v.back();
+    }
+    if (hipEventRecord(pick->fork, s) != hipSuccess || hipStreamWaitEvent(pick->h, pick->fork, 0) != hipSuccess)
+        return TG_EHIP;
+    pick->busy = true;
+    *out = pick->h;
+    return TG_OK;
+}
+
+int helper_join(hipStream_t h, hipStream_t s) {
+    std::lock_guard<std::mutex> g(g_helper_mu);
+    for (auto& x : helper_list()) {
+        if (x.h != h || !x.busy) continue;
+        // on failure the helper stays busy: never handed out behind a join
+        // event that does not cover its work
+        if (hipEventRecord(x.join, h) != hipSuccess || hipStreamWaitEvent(s, x.join, 0) != hipSuccess)
+            return TG_EHIP;
+        x.busy = false;
+        x.last = s;
+        return TG_OK;
+    }
+    return TG_EINVAL;
+}
+
+void helper_totals(uint64_t* streams, uint64_t* busy) {
+    std::lock_guard<std::mutex> g(g_helper_mu);
+    *streams = helper_list().size();
+    *busy = 0;
+    for (const auto& x : helper_list()) *busy += x.busy;
+}
+
+// Frees every idle helper whose work has completed, and idle scratch
+// buffers down to ``keep`` bytes (tg_scratch_trim).
+void scratch_trim(size_t keep) {
+    {
+        std::lock_guard<std::mutex> g(g_scratch_mu);
+        trim_locked(keep);
+    }
+    std::lock_guard<std::mutex> g(g_helper_mu);
+    auto& v = helper_list();
+    for (size_t i = 0; i < v.size();) {
+        HelperStream& x = v[i];
+        if (x.busy || hipEventQuery(x.join) != hipSuccess || hipStreamQuery(x.h) != hipSuccess) {
+            ++i;
+            continue;
+        }
+        (void)hipStreamDestroy(x.h);
+        (void)hipEventDestroy(x.fork);
+        (void)hipEventDestroy(x.join);
+        v.erase(v.begin() + (std::ptrdiff_t)i);
+    }
 }
 
 // tg_version()'s text; a measurement build appends its flags (common.h).
@@ -902,6 +1060,17 @@ int tg_gather(const uint8_t* src, const uint64_t* src_off, const uint32_t* len, 
 int tg_scratch_info(uint64_t* bytes, uint64_t* buffers) {
     if (!bytes || !buffers) return fail(TG_EINVAL, "null argument");
     tg::scratch_totals(bytes, buffers);
+    return TG_OK;
+}
+
+int tg_scratch_trim(uint64_t keep_bytes) {
+    tg::scratch_trim((size_t)keep_bytes);
+    return TG_OK;
+}
+
+int tg_helper_info(uint64_t* streams, uint64_t* busy) {
+    if (!streams || !busy) return fail(TG_EINVAL, "null argument");
+    tg::helper_totals(streams, busy);
     return TG_OK;
 }
 

@@ -322,6 +322,16 @@ int lds_attr(const void* fn, int bytes);
 int stream_alloc(void** p, size_t bytes, hipStream_t s);
 int stream_free(void* p, hipStream_t s);
 void scratch_totals(uint64_t* bytes, uint64_t* buffers);   // tg_scratch_info
+void scratch_trim(size_t keep);                             // tg_scratch_trim
+
+// A helper stream beside caller stream ``s`` (api.hip pool): helper_fork
+// takes one (idle, or last used by ``s``) and makes it wait for the work
+// queued on ``s`` so far; *h = nullptr when ``s`` belongs to another device
+// than the current one (run everything on ``s`` then).  helper_join makes
+// ``s`` wait for the helper's work and gives the helper back.  0 or TG_EHIP.
+int helper_fork(hipStream_t s, hipStream_t* h);
+int helper_join(hipStream_t h, hipStream_t s);
+void helper_totals(uint64_t* streams, uint64_t* busy);
 
 // Compute units of the current device (grid size of the persistent kernels),
 // looked up once per device.

@@ -6,7 +6,7 @@ objects they return), with
 hand-written HIP kernels for gfx950 behind a C ABI (include/tlsgpu.h,
 libtlsgpu.so) called through ctypes.
 """
-from ._lib import TlsGpuError, device_count, get_option, load, options, scratch_info, set_option  # noqa: F401
+from ._lib import TlsGpuError, device_count, get_option, load, options, scratch_info, scratch_trim, helper_info, set_option  # noqa: F401
 from .aead import HipAESCCM, HipAESGCM, HipCHACHA20_POLY1305  # noqa: F401
 from .batch import KeyTable, make_batch, make_nonces, open_batch, seal_batch  # noqa: F401
 from .cipherfactory import (CIPHER_IMPLEMENTATIONS, createAESCCM, createAESCCM_8,  # noqa: F401

@@ -32,7 +32,7 @@ EXPORTS = ("tg_version", "tg_last_error", "tg_device_count", "tg_init", "tg_key_
            "tg_memcpy_d2h", "tg_stream_sync", "tg_seal_records", "tg_open_records",
            "tg_hkdf_expand_label", "tg_key_create_device", "tg_scan_records", "tg_gather",
            "tg_selftest_poly1305", "tg_selftest_ghash", "tg_set_option", "tg_get_option",
-           "tg_scratch_info")
+           "tg_scratch_info", "tg_scratch_trim", "tg_helper_info")
 
 TG_TLS12 = 0x0303
 TG_TLS13 = 0x0304
@@ -140,6 +140,8 @@ def load():
     l.tg_set_option.argtypes = [ctypes.c_char_p, i]
     l.tg_get_option.argtypes = [ctypes.c_char_p, ctypes.POINTER(ctypes.c_int)]
     l.tg_scratch_info.argtypes = [ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64)]
+    l.tg_scratch_trim.argtypes = [ctypes.c_uint64]
+    l.tg_helper_info.argtypes = [ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64)]
     for name in EXPORTS:
         if name not in ("tg_version", "tg_last_error"):
             getattr(l, name).restype = ctypes.c_int
@@ -200,6 +202,18 @@ def scratch_info():
     b, n = ctypes.c_uint64(0), ctypes.c_uint64(0)
     check(load().tg_scratch_info(ctypes.byref(b), ctypes.byref(n)))
     return b.value, n.value
+
+
+def scratch_trim(keep_bytes=0):
+    """Free idle launch scratch down to ``keep_bytes`` and idle helper streams (tg_scratch_trim)."""
+    check(load().tg_scratch_trim(int(keep_bytes)))
+
+
+def helper_info():
+    """(helper streams held, helper streams in use) (tg_helper_info)."""
+    s, b = ctypes.c_uint64(0), ctypes.c_uint64(0)
+    check(load().tg_helper_info(ctypes.byref(s), ctypes.byref(b)))
+    return s.value, b.value
 
 
 def device_count():

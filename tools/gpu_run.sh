@@ -16,6 +16,7 @@
 #                  -> kernel_stats.csv
 #   pmc            tools/pmc_full.sh passes of the headline kernels
 #   traffic        tools/traffic.sh FETCH_SIZE / WRITE_SIZE passes -> traffic.json
+#   memprobe       device memory per fresh stream by launch kind -> stream_mem.jsonl
 #   c4fetch        FETCH_SIZE / WRITE_SIZE passes over one config-4 seal + open
 #                  -> c4fetch<suffix>.txt (per-dispatch sums by kernel)
 #   ab=LIBA,LIBB   alternate two built libraries (tools/gpu_lib_ab.sh) -> ab.txt
@@ -77,6 +78,8 @@ for st0 in "$@"; do
       python3 tools/pmc_summary.py $O > $O/fetch$SUF.txt 2>&1 || true; head -40 $O/fetch$SUF.txt ;;
     traffic)
       bash tools/traffic.sh $T ;;
+    memprobe)   # device memory per fresh stream by launch kind (tools/stream_mem_probe.py)
+      timeout -k 10 300 python -u tools/stream_mem_probe.py > $O/stream_mem.jsonl 2> $O/stream_mem.err; cat $O/stream_mem.jsonl ;;
     c4fetch)
       for c in FETCH_SIZE WRITE_SIZE; do
         (cd /tmp && export TMPDIR=/tmp && timeout -k 10 240 rocprofv3 --pmc $c --kernel-trace --output-format csv \
