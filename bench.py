@@ -323,6 +323,12 @@ def main():
                     help="config 4: pack records longest first on the host")
     ap.add_argument("--ingest-mib", type=int, default=2048,
                     help="application data per direction for --config ingest")
+    ap.add_argument("--ingest-batch", type=int, default=2048,
+                    help="--config ingest: records per pipeline batch (writer and reader)")
+    ap.add_argument("--ingest-slots", type=int, default=4,
+                    help="--config ingest: pipeline slots per direction")
+    ap.add_argument("--ingest-read-mib", type=int, default=512,
+                    help="--config ingest: bytes per socket read handed to the reader")
     args = ap.parse_args()
     if args.gpus < 1:
         ap.error("--gpus must be >= 1")
@@ -1184,14 +1190,15 @@ def run_ingest(args):
         mv = memoryview(data)
         # warm-up: build the wire stream once (also the reader's input)
         ms = _MemSink()
-        w = tlsgpu.RecordWriter(ms, obj(), tlsgpu.TLS13, iv, batch_records=8192)
+        w = tlsgpu.RecordWriter(ms, obj(), tlsgpu.TLS13, iv, batch_records=2048)
         for p in range(0, len(data), 64 << 20):
             w.write(mv[p:p + (64 << 20)])
         w.flush()
         wire = b"".join(ms.parts)
         del ms
         ns = _NullSink()
-        w = tlsgpu.RecordWriter(ns, obj(), tlsgpu.TLS13, iv, batch_records=8192)
+        w = tlsgpu.RecordWriter(ns, obj(), tlsgpu.TLS13, iv, batch_records=args.ingest_batch,
+                                nslots=args.ingest_slots)
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         for p in range(0, len(data), 64 << 20):
@@ -1200,28 +1207,56 @@ def run_ingest(args):
         t_w = time.perf_counter() - t0
         wv = memoryview(wire)
         rates, ok = {}, ns.bytes == len(wire)
-        # the caller's buffer pinned (packed plaintext lands in it by DMA) or pageable
-        for kind in ("pinned", "pageable"):
-            outbuf = (torch.empty(total, dtype=torch.uint8).pin_memory().numpy() if kind == "pinned"
-                      else np.empty(total, np.uint8))
-            r = tlsgpu.RecordReader(obj(), tlsgpu.TLS13, iv, batch_records=2048,
-                                    buffer_bytes=160 << 20)
+        # the caller's buffer pinned (packed plaintext lands in it by DMA) or
+        # pageable; socket reads of 128 MiB handed to read_application_data
+        # (data=: copied into the pinned buffer a batch at a time while the
+        # batches before run), or fed first (feed(): one threaded copy, then
+        # the pipeline)
+        for kind in ("pinned", "pageable", "pinned_feed"):
+            outbuf = (np.empty(total, np.uint8) if kind == "pageable"
+                      else torch.empty(total, dtype=torch.uint8).pin_memory().numpy())
+            rd = args.ingest_read_mib << 20
+            r = tlsgpu.RecordReader(obj(), tlsgpu.TLS13, iv, batch_records=args.ingest_batch,
+                                    buffer_bytes=rd + (32 << 20), nslots=args.ingest_slots)
             ov, pos = memoryview(outbuf), 0
             t0 = time.perf_counter()
-            for p in range(0, len(wire), 128 << 20):   # socket reads of 128 MiB
-                r.feed(wv[p:p + (128 << 20)])
-                pos += len(r.read_application_data(out=ov[pos:]))
+            for p in range(0, len(wire), rd):   # socket reads of --ingest-read-mib
+                if kind == "pinned_feed":
+                    r.feed(wv[p:p + rd])
+                    pos += len(r.read_application_data(out=ov[pos:]))
+                else:
+                    pos += len(r.read_application_data(out=ov[pos:], data=wv[p:p + rd]))
             rates[kind] = round(total / (time.perf_counter() - t0) / 2 ** 30, 2)
             ok = ok and pos == total and hashlib.sha256(outbuf).hexdigest() == want
             del r, ov, outbuf
         res[alg] = {"write_GiBps": round(total / t_w / 2 ** 30, 2),
                     "read_GiBps": rates["pinned"], "read_pageable_out_GiBps": rates["pageable"],
+                    "read_feed_first_GiBps": rates["pinned_feed"],
                     "records": w.records_sent, "wire_bytes": len(wire), "verified": ok}
         del wire
+    # the bounds beside it: pinned host <-> device copies, and host copies
+    # into pinned memory on 1 and on the pipeline's threads (tg_host_copy)
+    from tlsgpu import ingest as _ing
+    pin = torch.empty(1 << 30, dtype=torch.uint8).pin_memory().numpy()
+    page = np.frombuffer(blk * 16, np.uint8)
+    hc = {}
+    for th in (1, _ing.COPY_THREADS):
+        keep, _ing.COPY_THREADS = _ing.COPY_THREADS, th
+        _ing.host_copy(pin, page)
+        t0 = time.perf_counter()
+        for _ in range(3):
+            _ing.host_copy(pin, page)
+        hc["threads_%d" % th] = round(3 * (1 << 30) / (time.perf_counter() - t0) / 2 ** 30, 2)
+        _ing.COPY_THREADS = keep
+    del pin, page
     line = {"metric": "GiB/s host ingest pipeline (RecordWriter / RecordReader), TLS 1.3, "
                       "16 KiB records, host memory to host memory",
             "unit": "GiB/s", "n_gpus": 1, "app_data_bytes": total, "dtype": "u8",
-            "data": "synthetic", "per_alg": res}
+            "data": "synthetic", "per_alg": res, "pcie_GBps": pcie_ceiling(torch),
+            "pipeline": {"batch_records": args.ingest_batch, "slots": args.ingest_slots,
+                         "socket_read_bytes": args.ingest_read_mib << 20,
+                         "copy_threads": _ing.COPY_THREADS},
+            "host_copy_to_pinned_GiBps": hc}
     emit(line)
 
 

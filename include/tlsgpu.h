@@ -273,6 +273,16 @@ int64_t tg_scan_records(const uint8_t* buf, size_t len, uint32_t max_body, uint6
                         uint32_t* rlen, size_t max_n, size_t* consumed);
 int tg_gather(const uint8_t* src, const uint64_t* src_off, const uint32_t* len, uint8_t* dst,
               const uint64_t* dst_off, uint64_t n, void* stream);
+/* tg_host_copy / tg_host_copy_rows (HOST memory, no GPU): the ingest
+ *   pipeline's copies between callers' buffers and pinned staging, split over
+ *   up to nthreads threads (the caller plus a shared pool of workers;
+ *   nthreads <= 0 = min(8, hardware threads)).  rows: row r of row_bytes
+ *   bytes goes from src + r * src_stride to dst + r * dst_stride.  Regions
+ *   must not overlap.  Returns TG_OK or TG_EINVAL (NULL with a non-zero
+ *   size). */
+int tg_host_copy(void* dst, const void* src, size_t bytes, int nthreads);
+int tg_host_copy_rows(void* dst, size_t dst_stride, const void* src, size_t src_stride, size_t row_bytes,
+                      size_t rows, int nthreads);
 /* Self-test entry points (TEST-ONLY, not on the record path): run the
  * engine's device Poly1305 / GHASH arithmetic on raw messages, HOST buffers,
  * synchronous, so the reference's known answers reach the exact device code

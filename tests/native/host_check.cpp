@@ -19,6 +19,7 @@
 #include <string.h>
 
 #include <random>
+#include <thread>
 #include <vector>
 
 #include "host.h"
@@ -218,7 +219,45 @@ static int fuzz(long iters, uint64_t seed) {
     return g_fail;
 }
 
+// tg::host::parallel_copy(_rows) (hostcopy.cpp) into exactly-sized heap
+// buffers: every split (one row by bytes, rows contiguous and strided, 1 to
+// 12 threads, sizes around the 1 MiB chunk and 4 KiB boundaries) against a
+// plain memcpy, from two threads at once so the shared pool serves both.
+static int check_copy() {
+    std::mt19937_64 rng(99);
+    int fails = 0;
+    auto one = [&](uint64_t seed) {
+        std::mt19937_64 r(seed);
+        int f = 0;
+        for (int it = 0; it < 40; ++it) {
+            const size_t rows = r() % 3 == 0 ? 1 : 1 + r() % 700;
+            const size_t row = rows == 1 ? (r() % 2 ? (1u << 20) * (1 + r() % 5) + r() % 9000 : r() % 70000)
+                                         : 1 + r() % 20000;
+            const size_t ss = row + (r() % 2 ? 0 : r() % 64), ds = row + (r() % 2 ? 0 : r() % 64);
+            const size_t slen = rows ? (rows - 1) * ss + row : 0, dlen = rows ? (rows - 1) * ds + row : 0;
+            std::vector<uint8_t> src(slen), dst(dlen, 0xee), want(dlen, 0xee);
+            for (auto& x : src) x = (uint8_t)r();
+            for (size_t q = 0; q < rows; ++q) memcpy(want.data() + q * ds, src.data() + q * ss, row);
+            const int nt = 1 + (int)(r() % 12);
+            tg::host::parallel_copy_rows(dst.data(), ds, src.data(), ss, row, rows, nt);
+            if (dst != want) {
+                printf("copy mismatch rows %zu row %zu threads %d\n", rows, row, nt);
+                ++f;
+            }
+        }
+        return f;
+    };
+    int f1 = 0;
+    std::thread t([&] { f1 = one(rng()); });
+    fails += one(rng());
+    t.join();
+    fails += f1;
+    if (!fails) printf("copy ok\n");
+    return fails;
+}
+
 int main(int argc, char** argv) {
+    if (argc >= 2 && !strcmp(argv[1], "copy")) return check_copy() ? 1 : 0;
     if (argc >= 2 && !strcmp(argv[1], "keys")) {
         const int f = check_keys();
         if (!f) printf("keys ok\n");

@@ -272,3 +272,91 @@ def test_read_application_data_out_too_small_retry(torch, tg, out_kind, batch):
     assert bytes(big[:pos]) == want
     with pytest.raises(TLSBadRecordMAC):
         r.read_application_data(out=memoryview(big)[pos:])
+
+
+@pytest.mark.parametrize("ver,alg,klen,ivlen", SUITES[:3])
+def test_writer_write_buffer_commit(torch, tg, ver, alg, klen, ivlen):
+    """Zero-copy writes (write_buffer / commit): application data placed
+    straight into the pinned slot gives the same wire bytes as write() -- the
+    framing oracle's (oracle/records.py, pinned to the reference RecordLayer)
+    -- and the two can be mixed."""
+    key = detbytes("wb-key-" + alg, klen)
+    iv = detbytes("wb-iv-" + alg, ivlen)
+    version = tg.TLS13 if ver == "tls13" else tg.TLS12
+    limit = 2 ** 14
+    sink = Sink()
+    w = tg.RecordWriter(sink, _key(tg, alg, key), version, iv, seq0=3, batch_records=6)
+    msgs = _messages(3 * klen)
+    frags = []
+    for i, m in enumerate(msgs):
+        if i % 2:
+            w.write(m)
+            frags += _fragments([m], limit)
+            continue
+        pos = 0
+        while True:   # as much as the slot takes per commit (a socket recv_into loop)
+            buf = w.write_buffer()
+            k = min(len(buf), len(m) - pos)
+            buf[:k] = m[pos:pos + k]
+            w.commit(k)
+            frags += _fragments([m[pos:pos + k]], limit)
+            pos += k
+            if pos >= len(m):
+                break
+    w.flush()
+    want = b"".join(orec.seal_record(ver, alg, key, iv, 3 + i, 23, f) for i, f in enumerate(frags))
+    assert w.records_sent == len(frags)
+    assert bytes(sink.buf) == want
+    with pytest.raises(ValueError):
+        w.commit(10 ** 9)
+
+
+@pytest.mark.parametrize("batch", [2, 5, 1024])
+def test_read_application_data_with_data(torch, tg, batch):
+    """read_application_data(out, data=...): the wire bytes handed to the call
+    (copied batch by batch while the GPU opens the batches before) give the
+    same application data as feed() + read, across uneven socket reads and
+    records split between calls; recv_buffer / commit feeds in place."""
+    key, iv = detbytes("data-key", 16), detbytes("data-iv", 12)
+    recs, app = _mixed_stream(key, iv, 57, 11 + batch)
+    wire, want = b"".join(recs), b"".join(app)
+    for mode in ("data", "recv_buffer"):
+        r = tg.RecordReader(_key(tg, "aesgcm", key), tg.TLS13, iv, batch_records=batch)
+        buf = torch.empty(len(want) + 64, dtype=torch.uint8).pin_memory().numpy()
+        pos, rng, fed = 0, random.Random(batch), 0
+        while fed < len(wire):
+            k = rng.choice([3, 700, 20000, 100000, 300000, 10 ** 6])
+            piece = wire[fed:fed + k]
+            fed += k
+            if mode == "data":
+                pos += len(r.read_application_data(out=memoryview(buf)[pos:], data=piece))
+            else:
+                mv = r.recv_buffer(len(piece))
+                mv[:len(piece)] = piece
+                r.commit(len(piece))
+                pos += len(r.read_application_data(out=memoryview(buf)[pos:]))
+        assert bytes(buf[:pos]) == want, mode
+
+
+def test_read_application_data_with_data_errors(torch, tg):
+    """data= keeps the error contract: the application data before a bad tag,
+    then TLSBadRecordMAC; a too-small ``out`` is a ValueError that consumes
+    nothing of ``data`` (a retry with the same bytes and a larger buffer
+    returns them)."""
+    from tlsgpu.ingest import TLSBadRecordMAC
+    key, iv = detbytes("data-err", 16), detbytes("data-err-iv", 12)
+    recs, app = _mixed_stream(key, iv, 20, 5, bad=15)
+    r = tg.RecordReader(_key(tg, "aesgcm", key), tg.TLS13, iv, batch_records=3)
+    piece = b"".join(recs[:10])
+    first = b"".join(app[:10])
+    if first:
+        small = np.zeros(max(1, len(first) // 3), np.uint8)
+        with pytest.raises(ValueError):
+            r.read_application_data(out=memoryview(small), data=piece)
+    big = np.zeros(len(b"".join(app)) + 64, np.uint8)
+    pos = len(r.read_application_data(out=memoryview(big), data=piece))
+    assert bytes(big[:pos]) == first
+    pos += len(r.read_application_data(out=memoryview(big)[pos:], data=b"".join(recs[10:])))
+    assert bytes(big[:pos]) == b"".join(app[:15])
+    with pytest.raises(TLSBadRecordMAC):
+        r.read_application_data(out=memoryview(big)[pos:])

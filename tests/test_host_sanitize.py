@@ -26,10 +26,11 @@ def host_check(tmp_path_factory):
     if not shutil.which("g++"):
         pytest.skip("g++ not available")
     exe = str(tmp_path_factory.mktemp("asan") / "host_check")
-    cmd = ["g++", "-std=c++17", "-O1", "-g", "-fsanitize=address,undefined",
+    cmd = ["g++", "-std=c++17", "-O1", "-g", "-pthread", "-fsanitize=address,undefined",
            "-fno-sanitize-recover=all", "-fno-omit-frame-pointer", "-Wall", "-Wextra", "-Werror",
            "-I" + CSRC, "-I" + os.path.join(ROOT, "include"), "-o", exe,
-           os.path.join(HERE, "native", "host_check.cpp"), os.path.join(CSRC, "host.cpp")]
+           os.path.join(HERE, "native", "host_check.cpp"), os.path.join(CSRC, "host.cpp"),
+           os.path.join(CSRC, "hostcopy.cpp")]
     subprocess.run(cmd, check=True, capture_output=True, timeout=300)
     return exe
 
@@ -50,6 +51,13 @@ def test_sanitizer_is_live(host_check):
     assert r.returncode not in (0, 3, 4)
     # UBSan's object-size check or ASan's heap-buffer-overflow, whichever fires first
     assert b"heap-buffer-overflow" in r.stderr or b"insufficient space" in r.stderr
+
+
+def test_parallel_copy_clean(host_check):
+    """tg_host_copy(_rows)'s splits (hostcopy.cpp) against memcpy, two callers at once."""
+    r = _run(host_check, "copy")
+    assert r.returncode == 0, (r.stdout.decode()[-2000:], r.stderr.decode()[-3000:])
+    assert b"copy ok" in r.stdout
 
 
 def test_key_setup_clean(host_check):

@@ -75,6 +75,49 @@ __device__ __forceinline__ uint32_t wave_min_u32(uint32_t v) {
     return __builtin_amdgcn_readfirstlane(v);
 }
 
+// Measurement build TG_ROLE_PROBE (tools/role_probe.py): wave-cycles of the
+// single-key hybrid's octet jobs by role and phase, from s_memtime stamps at
+// the phase boundaries -- 0 record setup (counter cache / first-state planes,
+// AAD GHASH), 1 keystream (T-table halves / bitsliced cipher), 2 consume
+// (payload loads, XOR, stores, GHASH chain), 3 tail (length block, lift,
+// reduction, tag), 4 queue grab (the atomicAdd, gcm_hy_kernel) -- plus jobs,
+// blocks, and each wave's span from its first grab to its exit.  Summed over
+// the dispatch with atomics; printed by role_probe_print.
+#if defined(TG_ROLE_PROBE)
+__device__ unsigned long long g_rp[2][10];   // [T-table role][phase 0-4, jobs, blocks, span, waves, spare]
+struct RoleProbe {
+    uint64_t last = 0;
+    uint64_t acc[4] = {0, 0, 0, 0};
+    __device__ __forceinline__ void start() { last = __builtin_amdgcn_s_memtime(); }
+    __device__ __forceinline__ void mark(int k) {
+        const uint64_t t = __builtin_amdgcn_s_memtime();
+        acc[k] += t - last;
+        last = t;
+    }
+    __device__ __forceinline__ void flush(bool trole, uint32_t blocks) {
+        if ((threadIdx.x & 63u) == 0) {
+            for (int k = 0; k < 4; ++k) atomicAdd(&g_rp[trole][k], (unsigned long long)acc[k]);
+            atomicAdd(&g_rp[trole][5], 1ull);
+            atomicAdd(&g_rp[trole][6], (unsigned long long)blocks);
+        }
+    }
+};
+__global__ void role_probe_print() {
+    for (int r = 0; r < 2; ++r) {
+        printf("ROLE_PROBE role %s setup %llu cipher %llu consume %llu tail %llu grab %llu jobs %llu blocks %llu span %llu waves %llu\n",
+               r ? "ttable" : "bitsliced", g_rp[r][0], g_rp[r][1], g_rp[r][2], g_rp[r][3], g_rp[r][4], g_rp[r][5],
+               g_rp[r][6], g_rp[r][7], g_rp[r][8]);
+        for (int k = 0; k < 10; ++k) g_rp[r][k] = 0;
+    }
+}
+#else
+struct RoleProbe {
+    __device__ __forceinline__ void start() {}
+    __device__ __forceinline__ void mark(int) {}
+    __device__ __forceinline__ void flush(bool, uint32_t) {}
+};
+#endif
+
 // The T-table keystream of half h of a lane's batch: counters c0 + 8 j,
 // j = 4 h .. 4 h + 3, in lock step (one round-key read per round for the four), through
 // the 256-counter window cache (aes_round.h) when no lane of the wave crosses
@@ -226,6 +269,8 @@ __device__ __forceinline__ void octet_job(const KC& kc, const tg_batch& b,
 #define TG_KT_SHORT_MAX 5   // A/B builds: 7 / 8 measured 0.5 % slower (profiles/r05/r5v/)
 #endif
     constexpr uint32_t kShortMax = TG_KT_SHORT_MAX;
+    RoleProbe pr;   // (measurement build TG_ROLE_PROBE; otherwise empty)
+    if constexpr (LPR == 8) pr.start();
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t l = lane & kM;
     const uint64_t t = t0 + (lane >> kS);
@@ -289,6 +334,7 @@ __device__ __forceinline__ void octet_job(const KC& kc, const tg_batch& b,
         const uint32_t m = alen - 16 * a < 16 ? alen - 16 * a : 16;
         y = kc.gmulx(y, load_partial(ad + 16 * a, m));
     }
+    if constexpr (LPR == 8) pr.mark(0);
 
     // the bitsliced cipher leaves out the last round key (folded into the XOR)
     // (KeyPlanesVec: by a vector load, so consume()'s 3-input XORs take it
@@ -411,7 +457,9 @@ __device__ __forceinline__ void octet_job(const KC& kc, const tg_batch& b,
                     const uint4 wch = winh ? win_consts<NR>(lane4, rkT, cc, ch) : make_uint4(0, 0, 0, 0);
                     t_half<NR, LPR>(lane4, rkT, cc, c0, winh, wch, k0w, h, ks);
                 }
+                if constexpr (LPR == 8) pr.mark(1);
                 consume(ks, blk0, 4 * h, std::integral_constant<int, 4>(), fast ? dp : nullptr);
+                if constexpr (LPR == 8) pr.mark(2);
                 __builtin_amdgcn_sched_barrier(0);
             }
         } else if (!OPEN && one) {
@@ -476,10 +524,22 @@ __device__ __forceinline__ void octet_job(const KC& kc, const tg_batch& b,
             uint4 ks[8];
 #pragma unroll
             for (int j = 0; j < 8; ++j) ks[j] = make_uint4(w[0][j], w[1][j], w[2][j], w[3][j]);
+            if constexpr (LPR == 8) pr.mark(1);
             consume(ks, blk0, 0, std::integral_constant<int, 8>(), pre ? dp : nullptr);
+            if constexpr (LPR == 8) pr.mark(2);
         }
     }
-    if (!__any(valid)) return;
+    if constexpr (LPR == 8) pr.mark(2);
+#if defined(TG_ROLE_PROBE)
+    uint32_t pblk = (valid && l == 0) ? nc : 0u;
+    for (int m = 8; m < 64; m <<= 1) pblk += (uint32_t)__shfl_xor((int)pblk, m, 64);
+#endif
+    if (!__any(valid)) {
+#if defined(TG_ROLE_PROBE)
+        if constexpr (LPR == 8) pr.flush(TROLE, pblk);
+#endif
+        return;
+    }
     // length block be64(8 alen) || be64(8 len) (aesgcm.py:64): the last position
     if (l == kM) {
         const uint64_t abits = (uint64_t)alen << 3, cbits = (uint64_t)len << 3;
@@ -505,6 +565,12 @@ __device__ __forceinline__ void octet_job(const KC& kc, const tg_batch& b,
     const bool tag_aligned = aligned && tail == 0;
     if (!OPEN) {
         if (valid && l == 0) store16(out + len, tag, tag_aligned);
+#if defined(TG_ROLE_PROBE)
+        if constexpr (LPR == 8) {
+            pr.mark(3);
+            pr.flush(TROLE, pblk);
+        }
+#endif
         return;
     }
     // open: compare before releasing (aesgcm.py:148-149, constanttime.py:209-218)
@@ -520,6 +586,12 @@ __device__ __forceinline__ void octet_job(const KC& kc, const tg_batch& b,
         for (uint32_t blk = rho; blk < nfull; blk += LPR) store16(out + 16u * blk, z, aligned);
         if (tail && (nfull & kM) == rho) store_partial(out + 16u * nfull, z, tail);
     }
+#if defined(TG_ROLE_PROBE)
+    if constexpr (LPR == 8) {
+        pr.mark(3);
+        pr.flush(TROLE, pblk);
+    }
+#endif
 }
 
 __device__ __forceinline__ void stage_sbox(uint32_t base) {
@@ -619,13 +691,24 @@ __global__ __launch_bounds__(THREADS) void gcm_hy_kernel(const GcmKeyDev* __rest
     const uint64_t njobs = (bp->n + 7) / 8;
     const uint32_t recw = kHyRecBase + wave * kRecArea;
     const uint4 jw = lds_u128(kHyJt + ((threadIdx.x & 15u) << 4));
+#if defined(TG_ROLE_PROBE)
+    const uint64_t rp_t0 = __builtin_amdgcn_s_memtime();
+    uint64_t rp_grab = 0;
+#define RP_GRAB_START const uint64_t rp_g0 = __builtin_amdgcn_s_memtime();
+#define RP_GRAB_END rp_grab += __builtin_amdgcn_s_memtime() - rp_g0;
+#else
+#define RP_GRAB_START
+#define RP_GRAB_END
+#endif
     if (wave < nt) {
         if (prio) __builtin_amdgcn_s_setprio(1);
         const RkLds rk{kHyRk, rkrot};
         for (;;) {
+            RP_GRAB_START
             uint32_t job = 0;
             if ((threadIdx.x & 63u) == 0) job = atomicAdd(queue, 1u);
             job = (uint32_t)__builtin_amdgcn_readfirstlane((int)job);
+            RP_GRAB_END
             if (job >= njobs) break;
             asm volatile("" ::: "memory");
             const tg_batch b = *bp;
@@ -639,9 +722,11 @@ __global__ __launch_bounds__(THREADS) void gcm_hy_kernel(const GcmKeyDev* __rest
         // profiles/r04/r4a/aes_ab.txt), so they are not used here.
         const RkLds none{0};
         for (;;) {
+            RP_GRAB_START
             uint32_t job = 0;
             if ((threadIdx.x & 63u) == 0) job = atomicAdd(queue, 1u);
             job = (uint32_t)__builtin_amdgcn_readfirstlane((int)job);
+            RP_GRAB_END
             if (job >= njobs) break;
             asm volatile("" ::: "memory");
             const tg_batch b = *bp;
@@ -653,6 +738,16 @@ __global__ __launch_bounds__(THREADS) void gcm_hy_kernel(const GcmKeyDev* __rest
 #if defined(TG_TAIL_PROBE)
     tail_probe_end(wave < nt);
 #endif
+#if defined(TG_ROLE_PROBE)
+    if ((threadIdx.x & 63u) == 0) {
+        const bool tr = wave < nt;
+        atomicAdd(&g_rp[tr][4], (unsigned long long)rp_grab);
+        atomicAdd(&g_rp[tr][7], (unsigned long long)(__builtin_amdgcn_s_memtime() - rp_t0));
+        atomicAdd(&g_rp[tr][8], 1ull);
+    }
+#endif
+#undef RP_GRAB_START
+#undef RP_GRAB_END
 }
 
 // Stream-ordered setup of the hybrid kernel's scratch: the job counter and a
@@ -728,6 +823,9 @@ int launch_hy_kernels(const GcmKeyDev* key, const tg_batch& b, hipStream_t s, co
                            s, key, (const tg_batch*)bcopy, order, queue, nt, prio, krows, rkrot, masks);
 #if defined(TG_TAIL_PROBE)
     hipLaunchKernelGGL(tail_probe_print, dim3(1), dim3(1), 0, s);
+#endif
+#if defined(TG_ROLE_PROBE)
+    hipLaunchKernelGGL(role_probe_print, dim3(1), dim3(1), 0, s);
 #endif
     return hipGetLastError() == hipSuccess ? TG_OK : TG_EHIP;
 }

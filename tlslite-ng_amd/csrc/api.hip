@@ -1057,6 +1057,21 @@ int tg_gather(const uint8_t* src, const uint64_t* src_off, const uint32_t* len, 
     return rc ? fail(rc, "gather kernel launch failed") : TG_OK;
 }
 
+int tg_host_copy(void* dst, const void* src, size_t bytes, int nthreads) {
+    if (bytes && (!dst || !src)) return fail(TG_EINVAL, "null buffer");
+    tg::host::parallel_copy(dst, src, bytes, nthreads);
+    return TG_OK;
+}
+
+int tg_host_copy_rows(void* dst, size_t dst_stride, const void* src, size_t src_stride, size_t row_bytes,
+                      size_t rows, int nthreads) {
+    if (rows && row_bytes && (!dst || !src)) return fail(TG_EINVAL, "null buffer");
+    if (rows > 1 && (dst_stride < row_bytes || src_stride < row_bytes)) return fail(TG_EINVAL, "stride below row");
+    tg::host::parallel_copy_rows(static_cast<uint8_t*>(dst), dst_stride, static_cast<const uint8_t*>(src),
+                                 src_stride, row_bytes, rows, nthreads);
+    return TG_OK;
+}
+
 int tg_scratch_info(uint64_t* bytes, uint64_t* buffers) {
     if (!bytes || !buffers) return fail(TG_EINVAL, "null argument");
     tg::scratch_totals(bytes, buffers);

@@ -23,7 +23,7 @@ namespace tg {
 // library unless TLSGPU_ALLOW_MEASUREMENT_BUILD=1.
 void note_measurement_build(const char* flag);
 #if defined(TG_CHACHA_NO_IO) || defined(TG_CHACHA_ILV) || defined(TG_KT_NO_GHASH) || \
-    defined(TG_KT_NO_BUILD) || defined(TG_NT_IO) || defined(TG_TAIL_PROBE)
+    defined(TG_KT_NO_BUILD) || defined(TG_NT_IO) || defined(TG_TAIL_PROBE) || defined(TG_ROLE_PROBE)
 namespace {
 struct MeasurementMark {
     MeasurementMark() {
@@ -44,6 +44,9 @@ struct MeasurementMark {
 #endif
 #if defined(TG_TAIL_PROBE)
         note_measurement_build("TG_TAIL_PROBE");
+#endif
+#if defined(TG_ROLE_PROBE)
+        note_measurement_build("TG_ROLE_PROBE");
 #endif
     }
 } g_measurement_mark;

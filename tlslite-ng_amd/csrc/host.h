@@ -61,5 +61,14 @@ struct ScanError {
 int64_t scan_records(const uint8_t* buf, size_t len, uint32_t max_body, uint64_t* off,
                      uint32_t* rlen, size_t max_n, size_t* consumed, ScanError* err);
 
+// Parallel host copies (hostcopy.cpp): ``rows`` rows of ``row`` bytes from
+// src + r * src_stride to dst + r * dst_stride, split over up to ``nthreads``
+// threads (the caller and a shared worker pool; <= 0: copy_threads_default()).
+// Regions must not overlap.  parallel_copy: one contiguous range.
+int copy_threads_default();
+void parallel_copy_rows(uint8_t* dst, size_t dst_stride, const uint8_t* src, size_t src_stride, size_t row,
+                        size_t rows, int nthreads);
+void parallel_copy(void* dst, const void* src, size_t bytes, int nthreads);
+
 }  // namespace host
 }  // namespace tg

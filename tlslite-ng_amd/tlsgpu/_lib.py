@@ -32,7 +32,7 @@ EXPORTS = ("tg_version", "tg_last_error", "tg_device_count", "tg_init", "tg_key_
            "tg_memcpy_d2h", "tg_stream_sync", "tg_seal_records", "tg_open_records",
            "tg_hkdf_expand_label", "tg_key_create_device", "tg_scan_records", "tg_gather",
            "tg_selftest_poly1305", "tg_selftest_ghash", "tg_set_option", "tg_get_option",
-           "tg_scratch_info", "tg_scratch_trim", "tg_helper_info")
+           "tg_scratch_info", "tg_scratch_trim", "tg_helper_info", "tg_host_copy", "tg_host_copy_rows")
 
 TG_TLS12 = 0x0303
 TG_TLS13 = 0x0304
@@ -141,6 +141,8 @@ def load():
     l.tg_get_option.argtypes = [ctypes.c_char_p, ctypes.POINTER(ctypes.c_int)]
     l.tg_scratch_info.argtypes = [ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64)]
     l.tg_scratch_trim.argtypes = [ctypes.c_uint64]
+    l.tg_host_copy.argtypes = [p, p, sz, i]
+    l.tg_host_copy_rows.argtypes = [p, sz, p, sz, sz, sz, i]
     l.tg_helper_info.argtypes = [ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64)]
     for name in EXPORTS:
         if name not in ("tg_version", "tg_last_error"):

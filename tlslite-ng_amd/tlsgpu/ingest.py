@@ -18,12 +18,21 @@ records.py, for the bulk data of one connection direction.
   (tg_open_records) and returned in order as ``(content_type, bytearray)``;
   the first failing record raises the reference's exception.
 
-Each direction keeps ``nslots`` slots (writer 2, reader 3 by default), each
-with its own HIP stream: while one batch runs host->device copy, kernels and
-device->host copy, the host fills the next slot (writer); the reader's bulk
-path opens batch k+1 while batch k is packed and copied back (both PCIe
-directions busy at once).  Sequence numbers run on from ``seq0`` as in
+Each direction keeps ``nslots`` slots (3 by default), each with its own HIP
+stream: while one batch runs host->device copy, kernels and device->host
+copy, the host fills the next slot (writer); the reader's bulk path opens
+batch k+1 while batch k is packed and copied back (both PCIe directions busy
+at once).  Sequence numbers run on from ``seq0`` as in
 ConnectionState.getSeqNumBytes (:251-256).
+
+Host copies (application data into the writer's pinned slot, socket bytes
+into the reader's pinned buffer) go through ``tg_host_copy``: split over a
+pool of native threads, the GIL released.  Callers that can produce the
+bytes in place skip the copy: ``RecordWriter.write_buffer`` / ``commit``
+hand out the pinned slot itself, ``RecordReader.recv_buffer`` / ``commit``
+the reader's pinned buffer (e.g. for ``socket.recv_into``).  And
+``RecordReader.read_application_data(out, data=...)`` copies the socket bytes
+batch by batch while the batches before run on the GPU.
 """
 import ctypes
 
@@ -72,6 +81,25 @@ def _ru(x, m):
     return (x + m - 1) // m * m
 
 
+# threads of the host copies (tg_host_copy; 0 = the library's default); the
+# GPU box gives a process 16 cores
+COPY_THREADS = 12
+
+
+def _addr(a):
+    """Host address of a numpy array / pinned CPU tensor."""
+    return a.ctypes.data if isinstance(a, np.ndarray) else a.data_ptr()
+
+
+def host_copy(dst, src, nbytes=None):
+    """dst[:n] = src[:n] for host numpy arrays (or pinned CPU tensors) through
+    tg_host_copy: native threads, GIL released."""
+    n = len(src) if nbytes is None else int(nbytes)
+    if n == 0:
+        return
+    _lib.check(_lib.load().tg_host_copy(_addr(dst), _addr(src), n, COPY_THREADS))
+
+
 def _explicit_nonce(version, key):
     # TLS 1.2 AES-GCM / AES-CCM carry an 8-byte explicit nonce ("aes" in name)
     return 8 if version == TLS12 and "aes" in key.name else 0
@@ -80,10 +108,12 @@ def _explicit_nonce(version, key):
 class _Slot(object):
     """Pinned host + device buffers and a stream for one batch in flight."""
 
-    def __init__(self, torch, nrec, data_stride, wire_stride, wire_lead):
+    def __init__(self, torch, nrec, data_stride, wire_stride, wire_lead, app_bytes=0):
         self.stream = torch.cuda.Stream()
         self.event = torch.cuda.Event()
-        self.busy = False
+        self.app_event = torch.cuda.Event()   # the writer's h_app has gone to the device
+        self.busy = False        # wire output of the slot's last launch not yet sent
+        self.filling = False     # the writer's h_app still in use by a launch
         u8 = torch.uint8
         self.h_data = torch.empty(nrec * data_stride, dtype=u8).pin_memory()
         self.h_wire = torch.empty(nrec * wire_stride, dtype=u8).pin_memory()
@@ -103,8 +133,14 @@ class _Slot(object):
         idx = torch.arange(nrec, dtype=torch.int64, device="cuda")
         self.d_data_off = idx * data_stride
         self.d_wire_off = idx * wire_stride + wire_lead
+        if app_bytes:   # the writer's application data, contiguous
+            self.h_app = torch.empty(app_bytes, dtype=u8).pin_memory()
+            self.d_app = torch.empty(app_bytes, dtype=u8, device="cuda")
+            self.h_app_off = torch.empty(nrec, dtype=torch.int64).pin_memory()
+            self.d_app_off = torch.empty(nrec, dtype=torch.int64, device="cuda")
         self.n = 0
         self.nbytes = 0
+        self.app = 0
 
 
 class RecordWriter(object):
@@ -116,10 +152,16 @@ class RecordWriter(object):
     :param version: TLS12 or TLS13 (records.py)
     :param fixed_iv: ConnectionState.fixedNonce (12 bytes, or 4 for TLS 1.2
         AES-GCM / AES-CCM)
+
+    A slot holds the application data of up to ``batch_records`` records
+    contiguously in pinned memory; at launch it goes to the device in one
+    copy, is spread into the 16-byte aligned rows that tg_seal_records seals
+    in place (tg_gather), sealed, packed into one wire stream and copied
+    back.
     """
 
     def __init__(self, sink, key, version, fixed_iv, seq0=0, send_record_limit=2 ** 14,
-                 batch_records=1024, nslots=2, pad=0):
+                 batch_records=1024, nslots=3, pad=0):
         import torch
         if version not in (TLS12, TLS13):
             raise ValueError("version must be TLS12 or TLS13")
@@ -139,11 +181,41 @@ class RecordWriter(object):
         # payload after header (+ explicit nonce) starts 16-byte aligned
         self.lead = _ru(self.hdr, 16) - self.hdr
         self.wire_stride = _ru(self.lead + self.hdr + inner + self.tag, 16)
-        self.slots = [_Slot(torch, self.batch, self.data_stride, self.wire_stride, self.lead)
-                      for _ in range(nslots)]
+        self.app_cap = self.batch * self.limit
+        self.slots = [_Slot(torch, self.batch, self.data_stride, self.wire_stride, self.lead,
+                            app_bytes=self.app_cap) for _ in range(nslots)]
         self.cur = 0
         self.records_sent = 0
         self.bytes_sent = 0
+
+    def _slot(self):
+        """The slot being filled.  Its h_app may be refilled once the copy of
+        its last launch's application data to the device has finished; its
+        wire output of that launch is sent before its next launch."""
+        s = self.slots[self.cur]
+        if s.filling:
+            s.app_event.synchronize()
+            s.filling = False
+        return s
+
+    def _records(self, s, nbytes, content_type):
+        """Cut nbytes of application data, just placed at s.h_app[s.app:],
+        into records of at most send_record_limit bytes (sendRecord per
+        write call)."""
+        k = min(-(-nbytes // self.limit), self.batch - s.n) if nbytes else 1
+        lens = np.full(k, self.limit, np.int32)
+        if nbytes:
+            lens[-1] = nbytes - (k - 1) * self.limit
+        else:
+            lens[0] = 0
+        offs = s.app + np.arange(k, dtype=np.int64) * self.limit
+        s.h_len.numpy()[s.n:s.n + k] = lens
+        s.h_ctype.numpy()[s.n:s.n + k] = content_type
+        s.h_app_off.numpy()[s.n:s.n + k] = offs
+        s.n += k
+        s.app += nbytes
+        if s.n == self.batch or s.app + self.limit > self.app_cap:
+            self._launch(s)
 
     # -- RecordLayer.sendRecord for application data, batched
     def write(self, data, content_type=APPLICATION_DATA):
@@ -154,38 +226,40 @@ class RecordWriter(object):
         src = np.frombuffer(mv, np.uint8)
         pos = 0
         while True:
-            s = self.slots[self.cur]
-            if s.busy:
-                self._finish(s)
-            hd = s.h_data.numpy()
-            # whole records: one strided copy for as many as fit in the slot
-            m = min((len(src) - pos) // self.limit, self.batch - s.n)
-            if m > 1:
-                o = s.n * self.data_stride
-                dst = hd[o:o + m * self.data_stride].reshape(m, self.data_stride)
-                dst[:, :self.limit] = src[pos:pos + m * self.limit].reshape(m, self.limit)
-                s.h_len.numpy()[s.n:s.n + m] = self.limit
-                s.h_ctype.numpy()[s.n:s.n + m] = content_type
-                s.n += m
-                pos += m * self.limit
-            else:
-                k = min(len(src) - pos, self.limit)
-                o = s.n * self.data_stride
-                hd[o:o + k] = src[pos:pos + k]
-                s.h_len.numpy()[s.n] = k
-                s.h_ctype.numpy()[s.n] = content_type
-                s.n += 1
-                pos += k
-            if s.n == self.batch:
-                self._launch(s)
+            s = self._slot()
+            # whole records while the slot has room: one (threaded) copy
+            room = min((self.batch - s.n) * self.limit, self.app_cap - s.app)
+            k = min(len(src) - pos, room)
+            if k:
+                host_copy(s.h_app.numpy()[s.app:], src[pos:], k)
+            self._records(s, k, content_type)
+            pos += k
             if pos >= len(src):
                 break
 
+    def write_buffer(self):
+        """Zero-copy write: a writable memoryview of the current slot's free
+        pinned space (at least one record's worth).  Put application data at
+        its start, then call ``commit(n)``."""
+        s = self._slot()
+        room = min((self.batch - s.n) * self.limit, self.app_cap - s.app)
+        return memoryview(s.h_app.numpy()[s.app:s.app + room])
+
+    def commit(self, nbytes, content_type=APPLICATION_DATA):
+        """Queue the ``nbytes`` bytes placed at the start of write_buffer()
+        as records (as write() would)."""
+        s = self.slots[self.cur]
+        room = min((self.batch - s.n) * self.limit, self.app_cap - s.app)
+        if s.filling or not 0 <= nbytes <= room:
+            raise ValueError("commit() without a matching write_buffer(), or too many bytes")
+        self._records(s, int(nbytes), content_type)
+
     def flush(self):
         """Seal what is queued and send everything in order."""
-        s = self.slots[self.cur]
-        if s.n and not s.busy:
+        s = self._slot()
+        if s.n:
             self._launch(s)
+        # the slot after the last launched one holds the oldest unsent output
         for k in range(len(self.slots)):
             s = self.slots[(self.cur + k) % len(self.slots)]
             if s.busy:
@@ -197,6 +271,8 @@ class RecordWriter(object):
 
     def _launch(self, s):
         torch = self.torch
+        if s.busy:   # its previous wire output goes out first (in launch order)
+            self._finish(s)
         n = s.n
         lens = s.h_len.numpy()[:n].astype(np.int64)
         wl = self._wire_len(lens)
@@ -207,11 +283,16 @@ class RecordWriter(object):
         s.nbytes = int(wl.sum())
         pad = None
         with torch.cuda.stream(s.stream):
-            used = (n - 1) * self.data_stride + int(lens[-1]) if n else 0
-            s.d_data[:used].copy_(s.h_data[:used], non_blocking=True)
+            if s.app:
+                s.d_app[:s.app].copy_(s.h_app[:s.app], non_blocking=True)
             s.d_len[:n].copy_(s.h_len[:n], non_blocking=True)
             s.d_ctype[:n].copy_(s.h_ctype[:n], non_blocking=True)
             s.d_pack_off[:n].copy_(s.h_pack[:n], non_blocking=True)
+            s.d_app_off[:n].copy_(s.h_app_off[:n], non_blocking=True)
+            s.app_event.record(s.stream)   # h_app and the row metadata may be refilled
+            # the fragments into their aligned rows (room for the inner type,
+            # padding and tag after each)
+            gather(s.d_app, s.d_app_off, s.d_len, s.d_data, s.d_data_off, n, stream=s.stream)
             if self.pad:
                 pad = torch.full((n,), self.pad, dtype=torch.int32, device="cuda")
             seal_records(self.key, self.version, self.fixed_iv, self.seq, n, s.d_data, s.d_data_off,
@@ -222,15 +303,16 @@ class RecordWriter(object):
             s.event.record(s.stream)
         s.keep = pad
         s.busy = True
+        s.filling = True
+        s.sent_n, s.n, s.app = n, 0, 0
         self.seq += n
         self.cur = (self.cur + 1) % len(self.slots)
 
     def _finish(self, s):
         s.event.synchronize()
         self.sink.sendall(memoryview(s.h_wire.numpy())[:s.nbytes])
-        self.records_sent += s.n
+        self.records_sent += s.sent_n
         self.bytes_sent += s.nbytes
-        s.n = 0
         s.busy = False
 
 
@@ -286,17 +368,35 @@ class RecordReader(object):
             s.d_src = torch.empty(self.batch, dtype=torch.int64, device="cuda")
             s.d_rl = torch.empty(self.batch, dtype=torch.int32, device="cuda")
         self.pending_error = None
+        self._pool = None
+
+    def _reserve(self, nbytes):
+        """Room for nbytes more in the pinned buffer (grows it if needed)."""
+        need = self.fill + nbytes
+        if need > self.h_buf.numel():
+            nb = self.torch.empty(max(need, 2 * self.h_buf.numel()), dtype=self.torch.uint8).pin_memory()
+            host_copy(nb.numpy(), self.h_buf.numpy(), self.fill)
+            self.h_buf = nb
 
     def feed(self, data):
         """Append wire bytes (grows the pinned buffer if needed)."""
         mv = memoryview(data).cast("B")
-        need = self.fill + len(mv)
-        if need > self.h_buf.numel():
-            nb = self.torch.empty(max(need, 2 * self.h_buf.numel()), dtype=self.torch.uint8).pin_memory()
-            nb[:self.fill].copy_(self.h_buf[:self.fill])
-            self.h_buf = nb
-        self.h_buf.numpy()[self.fill:need] = np.frombuffer(mv, np.uint8)
-        self.fill = need
+        self._reserve(len(mv))
+        host_copy(self.h_buf.numpy()[self.fill:], np.frombuffer(mv, np.uint8), len(mv))
+        self.fill += len(mv)
+
+    def recv_buffer(self, nbytes=1 << 20):
+        """Zero-copy feed: a writable memoryview of at least ``nbytes`` free
+        bytes of the pinned buffer, e.g. for ``sock.recv_into``; then
+        ``commit(n)`` with the bytes received."""
+        self._reserve(nbytes)
+        return memoryview(self.h_buf.numpy()[self.fill:])
+
+    def commit(self, nbytes):
+        """Account ``nbytes`` bytes written at the start of recv_buffer()."""
+        if not 0 <= nbytes <= self.h_buf.numel() - self.fill:
+            raise ValueError("commit() beyond the buffer")
+        self.fill += int(nbytes)
 
     def _scan(self, start=0):
         """tg_scan_records over h_buf[start:fill]: (records, bytes, error)."""
@@ -327,13 +427,17 @@ class RecordReader(object):
                 out.append((int(ct[i]), bytearray(ho[o:o + int(plen[i])].tobytes())))
         return out
 
-    def read_application_data(self, out=None):
+    def read_application_data(self, out=None, data=None):
         """The bulk path: the plaintext of every application-data record
         completed so far, concatenated (other content types are dropped, as a
         caller that reads only application data would), copied into ``out``
         (a writable buffer, filled from offset 0) or a new bytearray; returns
         that buffer's filled part (memoryview / bytearray).  Raises like
         records().
+
+        ``data``: wire bytes to feed first (as feed(data)), copied into the
+        pinned buffer a batch at a time while the batches before it are
+        opened and copied back, so the host copy overlaps the GPU work.
 
         Pipelined over ``nslots`` slots, each with its own stream: batch k+1's
         H2D copy and open run while batch k is packed on the device
@@ -348,6 +452,13 @@ class RecordReader(object):
         torch = self.torch
         dst = None if out is None else np.frombuffer(out, np.uint8)
         direct = dst is not None and len(dst) > 0 and torch.from_numpy(dst[:1]).is_pinned()
+        src, spos = None, 0
+        if data is not None:
+            src = np.frombuffer(memoryview(data).cast("B"), np.uint8)
+            self._reserve(len(src))      # no reallocation while copies from h_buf run
+        # bytes of wire data per batch the scan should have in front of it
+        chunk = self.batch * (5 + self.max_body)
+        fill_entry = self.fill
         pieces = []
         self._pos = 0
         self._got = False
@@ -357,8 +468,26 @@ class RecordReader(object):
         free = list(self.rslots)
         start = 0
         err = None
+        # ``data`` goes into the pinned buffer one chunk ahead, on a helper
+        # thread (tg_host_copy releases the GIL), while this thread scans,
+        # launches and waits for the batches before it
+        pend = None       # (future, bytes) of the chunk being copied to h_buf[fill:]
+
+        def kick():
+            nonlocal spos, pend
+            if pend is None and src is not None and spos < len(src):
+                k = min(len(src) - spos, chunk)
+                pend = (self._copier().submit(host_copy, self.h_buf.numpy()[self.fill:], src[spos:], k), k)
+                spos += k
+
         try:
             while not self._dead:
+                kick()
+                if pend is not None and self.fill - start < chunk:
+                    pend[0].result()
+                    self.fill += pend[1]
+                    pend = None
+                    continue
                 n, used, err = self._scan(start)
                 if n:
                     if not free:
@@ -371,11 +500,13 @@ class RecordReader(object):
                     meta.append(s)
                     if len(meta) > 1:
                         done.append(self._pack(meta.pop(0), dst, direct, pieces))
-                if err is not None or n < self.batch:
+                if err is not None or (n < self.batch and pend is None and (src is None or spos >= len(src))):
                     break
             while meta:
                 done.append(self._pack(meta.pop(0), dst, direct, pieces))
         except _OutTooSmall:
+            if pend is not None:
+                pend[0].result()
             # nothing of this call is delivered: wait for every slot still
             # running (opens, and copies into ``out``), then undo the call --
             # the sequence number and the wire bytes stay where they were, so
@@ -383,9 +514,13 @@ class RecordReader(object):
             for s in meta + done + self.rslots:
                 s.event.synchronize()
             self.seq = seq_entry
+            self.fill = fill_entry     # ``data`` was not consumed either
             self.pending_error = None
             self._dead = False
             raise ValueError("output buffer too small")
+        if pend is not None:   # (an error ended the loop with a chunk in flight)
+            pend[0].result()
+            self.fill += pend[1]
         while done:
             self._finish_read(done.pop(0), dst)
         # the unconsumed tail to the front (every copy from h_buf has finished)
@@ -409,6 +544,12 @@ class RecordReader(object):
         if len(pieces) == 1:
             return pieces[0]
         return bytearray(b"".join(pieces))
+
+    def _copier(self):
+        if self._pool is None:
+            import concurrent.futures
+            self._pool = concurrent.futures.ThreadPoolExecutor(1, thread_name_prefix="tlsgpu-recv")
+        return self._pool
 
     def _enqueue_open(self, s, start, n, used):
         """H2D of n scanned records (wire bytes h_buf[start:start+used]),

@@ -5,9 +5,11 @@
 // SIMD gives the issue rate.  hipcc -O3 --offload-arch=gfx950 -o tools/bank_probe tools/bank_probe.hip
 #include <hip/hip_runtime.h>
 #include <cstdio>
+#include <cstdlib>
 
 #define CLOB "v10", "v11", "v12", "v13", "v14", "v15", "v16", "v17", "v18", "v19", "v20", "v21", \
              "v22", "v23", "v24", "v25", "v26", "v27", "v28", "v29", "v30", "v31", "v32", "v33"
+// (the probes only read v20..v31: their values do not matter)
 
 // 8 independent instructions: dst v10..v17 (rotating), sources from v20..v27
 // same bank: (v20, v24) (v21, v25) (v22, v26) (v23, v27): n and n + 4
@@ -98,6 +100,66 @@ __global__ __launch_bounds__(512) void probe_sop(unsigned* out, int iters, unsig
     if (threadIdx.x == 0) out[blockIdx.x] = iters;
 }
 
+// v_bitop3_b32 with three VGPR sources (the S-box gates of aes_bs_sbox.h):
+// K 0 three banks, 1 two sources in one bank, 2 all three in one bank
+template <int K>
+__global__ __launch_bounds__(512) void probe_b3(unsigned* out, int iters) {
+    for (int i = 0; i < iters; ++i) {
+        if (K == 0)
+            asm volatile(".rept 32\n"
+                         "v_bitop3_b32 v10, v20, v21, v22 bitop3:0x96\n v_bitop3_b32 v11, v21, v22, v23 bitop3:0x96\n"
+                         "v_bitop3_b32 v12, v22, v23, v24 bitop3:0x96\n v_bitop3_b32 v13, v23, v24, v25 bitop3:0x96\n"
+                         "v_bitop3_b32 v14, v24, v25, v26 bitop3:0x96\n v_bitop3_b32 v15, v25, v26, v27 bitop3:0x96\n"
+                         "v_bitop3_b32 v16, v26, v27, v28 bitop3:0x96\n v_bitop3_b32 v17, v27, v28, v29 bitop3:0x96\n"
+                         ".endr\n" ::: CLOB);
+        if (K == 1)
+            asm volatile(".rept 32\n"
+                         "v_bitop3_b32 v10, v20, v24, v21 bitop3:0x96\n v_bitop3_b32 v11, v21, v25, v22 bitop3:0x96\n"
+                         "v_bitop3_b32 v12, v22, v26, v23 bitop3:0x96\n v_bitop3_b32 v13, v23, v27, v24 bitop3:0x96\n"
+                         "v_bitop3_b32 v14, v24, v28, v25 bitop3:0x96\n v_bitop3_b32 v15, v25, v29, v26 bitop3:0x96\n"
+                         "v_bitop3_b32 v16, v26, v30, v27 bitop3:0x96\n v_bitop3_b32 v17, v27, v31, v28 bitop3:0x96\n"
+                         ".endr\n" ::: CLOB);
+        if (K == 2)
+            asm volatile(".rept 32\n"
+                         "v_bitop3_b32 v10, v20, v24, v28 bitop3:0x96\n v_bitop3_b32 v11, v21, v25, v29 bitop3:0x96\n"
+                         "v_bitop3_b32 v12, v22, v26, v30 bitop3:0x96\n v_bitop3_b32 v13, v23, v27, v31 bitop3:0x96\n"
+                         "v_bitop3_b32 v14, v20, v24, v28 bitop3:0x96\n v_bitop3_b32 v15, v21, v25, v29 bitop3:0x96\n"
+                         "v_bitop3_b32 v16, v22, v26, v30 bitop3:0x96\n v_bitop3_b32 v17, v23, v27, v31 bitop3:0x96\n"
+                         ".endr\n" ::: CLOB);
+    }
+    if (threadIdx.x == 0) out[blockIdx.x] = iters;
+}
+
+// Dependent chains: C independent chains of v_bitop3 (VGPR sources, three
+// banks) per wave, each instruction reading its chain's previous result;
+// C = 1 / 2 / 4 / 8.  With W waves per SIMD this shows how much independent
+// work per wave the VALU needs to issue at its rate.
+template <int C>
+__global__ __launch_bounds__(256) void probe_chain(unsigned* out, int iters) {
+    for (int i = 0; i < iters; ++i) {
+        if (C == 1)
+            asm volatile(".rept 256\n v_bitop3_b32 v10, v10, v21, v22 bitop3:0x96\n .endr\n" ::: CLOB);
+        if (C == 2)
+            asm volatile(".rept 128\n v_bitop3_b32 v10, v10, v21, v22 bitop3:0x96\n"
+                         " v_bitop3_b32 v11, v11, v22, v23 bitop3:0x96\n .endr\n" ::: CLOB);
+        if (C == 4)
+            asm volatile(".rept 64\n v_bitop3_b32 v10, v10, v21, v22 bitop3:0x96\n"
+                         " v_bitop3_b32 v11, v11, v22, v23 bitop3:0x96\n"
+                         " v_bitop3_b32 v12, v12, v23, v24 bitop3:0x96\n"
+                         " v_bitop3_b32 v13, v13, v24, v25 bitop3:0x96\n .endr\n" ::: CLOB);
+        if (C == 8)
+            asm volatile(".rept 32\n v_bitop3_b32 v10, v10, v21, v22 bitop3:0x96\n"
+                         " v_bitop3_b32 v11, v11, v22, v23 bitop3:0x96\n"
+                         " v_bitop3_b32 v12, v12, v23, v24 bitop3:0x96\n"
+                         " v_bitop3_b32 v13, v13, v24, v25 bitop3:0x96\n"
+                         " v_bitop3_b32 v14, v14, v25, v26 bitop3:0x96\n"
+                         " v_bitop3_b32 v15, v15, v26, v27 bitop3:0x96\n"
+                         " v_bitop3_b32 v16, v16, v27, v28 bitop3:0x96\n"
+                         " v_bitop3_b32 v17, v17, v28, v29 bitop3:0x96\n .endr\n" ::: CLOB);
+    }
+    if (threadIdx.x == 0) out[blockIdx.x] = iters;
+}
+
 template <class F>
 float timeit(F f) {
     hipEvent_t a, b;
@@ -126,6 +188,26 @@ int main() {
         printf("%-34s %8.3f ms  %6.1f lane-ops/clk/CU (2.4 GHz)\n", name, ms,
                instr * 64 / (ms * 1e-3) / 2.4e9 / cus);
     };
+    if (getenv("BANK_PROBE_B3")) {   // the 3-source and dependency-chain probes only
+        for (int r = 0; r < 2; ++r) {
+            rep("v_bitop3 3 VGPRs, three banks", timeit([&] { probe_b3<0><<<blocks, 512>>>(out, iters); }));
+            rep("v_bitop3 3 VGPRs, two in one bank", timeit([&] { probe_b3<1><<<blocks, 512>>>(out, iters); }));
+            rep("v_bitop3 3 VGPRs, all in one bank", timeit([&] { probe_b3<2><<<blocks, 512>>>(out, iters); }));
+            // 256-thread workgroups: W waves per SIMD = blocks per CU
+            for (int w : {1, 2, 4, 8}) {
+                const double ins = (double)cus * w * 4 * iters * 256;   // wave instructions
+                auto rc = [&](const char* name, float ms) {
+                    printf("%-22s %d waves/SIMD %8.3f ms  %6.1f lane-ops/clk/CU (2.4 GHz)\n", name, w, ms,
+                           ins * 64 / (ms * 1e-3) / 2.4e9 / cus);
+                };
+                rc("bitop3 chains x1", timeit([&] { probe_chain<1><<<cus * w, 256>>>(out, iters); }));
+                rc("bitop3 chains x2", timeit([&] { probe_chain<2><<<cus * w, 256>>>(out, iters); }));
+                rc("bitop3 chains x4", timeit([&] { probe_chain<4><<<cus * w, 256>>>(out, iters); }));
+                rc("bitop3 chains x8", timeit([&] { probe_chain<8><<<cus * w, 256>>>(out, iters); }));
+            }
+        }
+        return 0;
+    }
     for (int r = 0; r < 2; ++r) {
         rep("v_xor_b32 same-bank sources", timeit([&] { probe<0><<<blocks, 512>>>(out, iters); }));
         rep("v_xor_b32 different-bank sources", timeit([&] { probe<1><<<blocks, 512>>>(out, iters); }));

@@ -17,6 +17,8 @@
 #   pmc            tools/pmc_full.sh passes of the headline kernels
 #   traffic        tools/traffic.sh FETCH_SIZE / WRITE_SIZE passes -> traffic.json
 #   memprobe       device memory per fresh stream by launch kind -> stream_mem.jsonl
+#   roleprobe      per-role cycle accounting of the hybrid AES-GCM kernel -> role_probe.json
+#   pmcroles       counters of the hybrid for three role mixes (tools/pmc_roles2.sh)
 #   c4fetch        FETCH_SIZE / WRITE_SIZE passes over one config-4 seal + open
 #                  -> c4fetch<suffix>.txt (per-dispatch sums by kernel)
 #   ab=LIBA,LIBB   alternate two built libraries (tools/gpu_lib_ab.sh) -> ab.txt
@@ -78,6 +80,10 @@ for st0 in "$@"; do
       python3 tools/pmc_summary.py $O > $O/fetch$SUF.txt 2>&1 || true; head -40 $O/fetch$SUF.txt ;;
     traffic)
       bash tools/traffic.sh $T ;;
+    roleprobe)   # per-role cycle accounting (tools/role_probe.py, tools/ab/role_probe.so) + role PMC passes
+      timeout -k 10 900 python -u tools/role_probe.py tools/ab/role_probe.so > $O/role_probe.json 2> $O/role_probe.err; tail -3 $O/role_probe.err ;;
+    pmcroles)
+      bash tools/pmc_roles2.sh $T/pmc_roles ;;
     memprobe)   # device memory per fresh stream by launch kind (tools/stream_mem_probe.py)
       timeout -k 10 300 python -u tools/stream_mem_probe.py > $O/stream_mem.jsonl 2> $O/stream_mem.err; cat $O/stream_mem.jsonl ;;
     c4fetch)
