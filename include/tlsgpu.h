@@ -82,7 +82,8 @@ int tg_init(int device);                   /* hipSetDevice for the calling threa
  *                      stream)
  *   chacha_variant     0 auto, 3 wave per record, 4 lane per record with
  *                      the register-staged tile, 5 lane per record with the
- *                      LDS-DMA tile (auto's choice for large batches)
+ *                      LDS-DMA tile (auto's choice for large batches),
+ *                      6 eight lanes per record (octets, single key)
  *   ccm_variant        0 auto, 1 lane full rounds, 2 wave, 3 lane, 4 hybrid
  *                      (bitsliced keystream + T-table MAC waves, single key),
  *                      5 / 6 / 7 / 8 lane with the payload 1 / 2 / 4 / 8
@@ -292,7 +293,8 @@ int tg_host_copy_rows(void* dst, size_t dst_stride, const void* src, size_t src_
  * tg_selftest_poly1305: tags[i] = Poly1305(keys[i] (32 B), msgs + off[i],
  *   len[i] bytes) with RFC padding; mode 0 = the lane Horner of the batch
  *   kernel, 1 / 2 / 3 = the wave-striped Horner of the wave-per-record
- *   kernel with 1 / 4 / 16 waves per message.
+ *   kernel with 1 / 4 / 16 waves per message, 4 = the octet striping of the
+ *   octet kernel (eight lanes per message, chacha_variant 6).
  * tg_selftest_ghash: out[i] = GHASH_H(aad_i, ct_i) (h: n x 16 B, GCM byte
  *   order); mode 0 = 8-bit tables, 1 = 8-bit tables 8 rows in flight,
  *   2 = conflict-free rotated tables, 3 = table-free carry-less multiply,

@@ -42,6 +42,7 @@ LENS = [0, 1, 15, 16, 17, 63, 64, 65, 1000, 1024, 1040, 4095, 16383, 16384, 1638
     ("chacha", 32, {"chacha_variant": 4}),        # lane per record, register-staged tile fill
     ("chacha", 32, {"chacha_variant": 5}),        # lane per record, LDS-DMA tile fill (auto)
     ("chacha", 32, {"chacha_variant": 3}),        # wave per record
+    ("chacha", 32, {"chacha_variant": 6}),        # eight lanes per record (octets), no tile
 ])
 @pytest.mark.parametrize("align", [16, 1])
 def test_forced_kernel_vs_oracle(torch, tg, oracle_mod, alg, klen, opts, align):
@@ -87,6 +88,7 @@ def test_auto_wave_per_record_batch(torch, tg, oracle_mod, alg, klen):
     ("aesgcm", 16, 1, {"gcm_variant": 16}), ("aesgcm", 16, 1, {"gcm_variant": 14}),
     ("aesgcm", 16, 1, {"gcm_variant": 15}), ("aesgcm", 32, 1, {"gcm_variant": 15}),
     ("chacha", 32, 1, {"chacha_variant": 4}), ("chacha", 32, 1, {"chacha_variant": 5}),
+    ("chacha", 32, 1, {"chacha_variant": 6}),
     ("chacha", 32, 29, {"chacha_variant": 4}),
     ("aesgcm", 32, 29, {"gcm_table_variant": 1}), ("aesgcm", 32, 29, {"gcm_table_variant": 0}),
     ("aesgcm", 16, 29, {"gcm_table_variant": 14}), ("chacha", 32, 29, {})])

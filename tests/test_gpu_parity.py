@@ -193,7 +193,7 @@ def test_config1_digest(torch, tg):
 # ------------------------------------------- full-size (BASELINE configs 2/3)
 
 @pytest.mark.parametrize("alg", ["aesgcm", "chacha", "aesgcm-bs8", "chacha-regs", "aesgcm-stride",
-                                 "chacha-stride"])
+                                 "chacha-stride", "chacha-octet", "chacha-octet-stride"])
 def test_full_size_roundtrip_and_samples(torch, tg, oracle_mod, alg):
     """2^20 x 16 KiB records: every record's ciphertext and tag bit-exact
     against the threaded C oracle (tests/fullcheck.py, 2^16-record chunks),
@@ -201,14 +201,15 @@ def test_full_size_roundtrip_and_samples(torch, tg, oracle_mod, alg):
     through the oracle's per-record entry point.
     aesgcm-bs8 forces the 8-block bitsliced kernel (gcm_variant 14),
     chacha-regs the register-staged tile fill (chacha_variant 4; the default
-    fills it by LDS-DMA).  *-stride: sealed records at bench.py's stride,
+    fills it by LDS-DMA), chacha-octet the octet kernel (chacha_variant 6,
+    eight lanes per record, no tile).  *-stride: sealed records at bench.py's stride,
     L + 16 rounded up to a 128-byte line (16 512 B), the layout the metric is
     measured on."""
     variant = 14 if alg == "aesgcm-bs8" else 0
-    cv = 4 if alg == "chacha-regs" else 0
+    cv = 4 if alg == "chacha-regs" else 6 if alg.startswith("chacha-octet") else 0
     stride = 16512 if alg.endswith("-stride") else None
     alg = {"aesgcm-bs8": "aesgcm", "chacha-regs": "chacha", "aesgcm-stride": "aesgcm",
-           "chacha-stride": "chacha"}.get(alg, alg)
+           "chacha-stride": "chacha", "chacha-octet": "chacha", "chacha-octet-stride": "chacha"}.get(alg, alg)
     with tg.options(gcm_variant=variant, chacha_variant=cv):
         _full_size(torch, tg, oracle_mod, alg, stride)
 

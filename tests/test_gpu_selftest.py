@@ -34,7 +34,7 @@ def _extra_msgs():
     return keys, msgs, tags
 
 
-@pytest.mark.parametrize("mode", [0, 1, 2, 3])
+@pytest.mark.parametrize("mode", [0, 1, 2, 3, 4])
 def test_poly1305_rfc7539_kats(st, mode):
     keys = [bytes.fromhex(v["key"]) for v in KAT]
     msgs = [bytes.fromhex(v["msg"]) for v in KAT]
@@ -43,7 +43,7 @@ def test_poly1305_rfc7539_kats(st, mode):
         assert got[i].hex() == v["tag"], (st.POLY_MODES[mode], i)
 
 
-@pytest.mark.parametrize("mode", [0, 1, 2, 3])
+@pytest.mark.parametrize("mode", [0, 1, 2, 3, 4])
 def test_poly1305_reduction_edges(st, mode):
     keys, msgs, tags = _extra_msgs()
     got = st.poly1305(mode, keys, msgs)
@@ -60,3 +60,22 @@ def test_ghash_reference_values(st, mode):
     got = st.ghash(mode, hs, aads, cts)
     for i, v in enumerate(vecs):
         assert got[i].hex() == v["ghash"], (st.GHASH_MODES[mode], v["h_label"], v["aad_len"], v["ct_len"])
+
+
+def test_poly1305_octet_striping_every_shape(st):
+    """The octet striping (mode 4: r within a 64-byte chunk, r^29 across the
+    other lanes' chunks, the lift r^(4 (d - 1) + mlast), the octet sum) on
+    every message length 0 .. 1200 and a spread of longer ones (all chunk
+    counts mod 8, every last-chunk fill), against the lane Horner (mode 0),
+    which the RFC 7539 vectors above pin."""
+    import random
+    rng = random.Random(4)
+    lens = list(range(0, 1201)) + [rng.randint(1201, 70000) for _ in range(200)]
+    keys = [bytes(detbytes("oct-key-%d" % i, 32)) for i in range(len(lens))]
+    keys[:4] = [b"\xff" * 32] * 4     # clamped-maximum r, s
+    msgs = [bytes(detbytes("oct-msg-%d" % i, n)) for i, n in enumerate(lens)]
+    msgs[:4] = [b"\xff" * n for n in lens[:4]]
+    a = st.poly1305(4, keys, msgs)
+    b = st.poly1305(0, keys, msgs)
+    bad = [i for i in range(len(lens)) if a[i] != b[i]]
+    assert not bad, [(i, lens[i]) for i in bad[:8]]

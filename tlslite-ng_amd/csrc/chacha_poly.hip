@@ -104,6 +104,15 @@ __device__ __forceinline__ uint32_t wave_min(uint32_t v) {
     return v;
 }
 
+__device__ __forceinline__ uint32_t wave_max_octet(uint32_t v) {
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t w = (uint32_t)__shfl_xor((int)v, o);
+        v = w > v ? w : v;
+    }
+    return (uint32_t)__builtin_amdgcn_readfirstlane((int)v);
+}
+
 // Per-wave LDS: a 64-record x 128-byte tile -- row r = the record of lane r,
 // holding one aligned pair of 64-byte blocks (one 128-byte HBM line) -- and
 // the records' in/out base pointers.  Chunk c of row r sits at 16-byte slot
@@ -597,6 +606,180 @@ __global__ __launch_bounds__(chacha_wave_threads<W>()) void chacha_wave_kernel(
     }
 }
 
+// ---- octet kernel: eight lanes per record, no LDS tile --------------------
+// (chacha_variant 6.)  Lane l of a record's octet takes
+// the ChaCha blocks b = l, l + 8, ... (counter b + 1): for a fixed load or
+// store instruction the octet's lanes touch 8 x 16 bytes of one 512-byte
+// stretch of the record, and the four instructions of a block complete its
+// 128-byte lines back to back -- no LDS round trip, no wave barriers.
+// Poly1305 runs per lane over the lane's own blocks (poly1305.h octet
+// striping: r within a block, r^29 across the other lanes' blocks, the lift
+// and the octet sum at the end), in 26-bit limbs.  The one-time key and the
+// powers of r come from chacha_otk_kernel (one lane per record, before).
+// Lane 0 of the octet also runs the AAD blocks, which precede its block 0
+// in mac_data (chacha20_poly1305.py:60-63).
+constexpr int kOctetThreads = 256;
+#if !defined(TG_OCTET_NT)   // A/B builds: non-temporal payload loads and stores
+#define TG_OCTET_NT 0
+#endif
+
+// Block 0 of every record (poly1305_key_gen, chacha20_poly1305.py:35-38):
+// r clamped, its powers and s, by slot t (record order[t] or t).
+__global__ __launch_bounds__(256) void chacha_otk_kernel(const ChachaKeyDev* __restrict__ key, tg_batch b,
+                                                         const uint32_t* __restrict__ order,
+                                                         OctetPoly* __restrict__ out) {
+    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= b.n) return;
+    const uint64_t i = order ? gld(order, t) : t;
+    uint32_t k[8];
+#pragma unroll
+    for (int w = 0; w < 8; ++w) k[w] = key->k[w];
+    const uint4 nv = load_partial(b.nonce + 12 * i, 12);
+    uint32_t otk[16];
+    chacha_block(k, 0, nv.x, nv.y, nv.z, otk);
+    Poly p;
+    poly_init(p, otk);
+    OctetPoly o;
+    octet_powers(F5{p.r0, p.r1, p.r2, p.r3, p.r4}, o);
+    o.s[0] = p.p0; o.s[1] = p.p1; o.s[2] = p.p2; o.s[3] = p.p3;
+    o.pad[0] = o.pad[1] = 0;
+    const uint32_t* w = reinterpret_cast<const uint32_t*>(&o);
+    uint8_t* dst = reinterpret_cast<uint8_t*>(out + t);
+#pragma unroll
+    for (int q = 0; q < 9; ++q) gstore16(dst + 16 * q, make_uint4(w[4 * q], w[4 * q + 1], w[4 * q + 2], w[4 * q + 3]));
+}
+
+template <bool OPEN>
+__global__ __launch_bounds__(kOctetThreads, 4) void chacha_octet_kernel(const ChachaKeyDev* __restrict__ key,
+                                                                        tg_batch b,
+                                                                        const uint32_t* __restrict__ order,
+                                                                        const OctetPoly* __restrict__ pw) {
+    const uint32_t lane = threadIdx.x & 63u, l = lane & 7u;
+    const uint64_t t = ((uint64_t)blockIdx.x * kOctetThreads + threadIdx.x) >> 3;
+    const uint64_t wave_first = ((uint64_t)blockIdx.x * kOctetThreads + (threadIdx.x & ~63u)) >> 3;
+    if (wave_first >= b.n) return;   // whole wave idle (uniform)
+    const bool valid = t < b.n;
+    const uint64_t i = valid ? (order ? gld(order, t) : t) : 0;
+    uint32_t k[8];
+#pragma unroll
+    for (int w = 0; w < 8; ++w) k[w] = key->k[w];
+    uint32_t len = 0, alen = 0;
+    const uint8_t* in = nullptr;
+    uint8_t* out = nullptr;
+    const uint8_t* ad = nullptr;
+    uint4 nv = make_uint4(0, 0, 0, 0);
+    const uint32_t* pwt = reinterpret_cast<const uint32_t*>(pw + (valid ? t : 0));
+    if (valid) {
+        len = rec_len(b, i);
+        alen = rec_aad_len(b, i);
+        in = rec_in(b, i);
+        out = rec_out(b, i);
+        ad = rec_aad(b, i);
+        nv = load_partial(b.nonce + 12 * i, 12);
+    }
+    const OctetPoly* op = reinterpret_cast<const OctetPoly*>(pwt);
+    const Mul26 R = mul26(f5_at(op->r)), R29 = mul26(f5_at(op->r29));
+    const uint32_t nch = (len + 63) >> 6;        // 64-byte chunks (ChaCha blocks) of the payload
+    const uint32_t nfull = len >> 6;             // full ones
+    F5 h = {0, 0, 0, 0, 0};
+    if (l == 0) {   // mac_data starts with the AAD (chacha20_poly1305.py:60)
+        for (uint32_t off = 0; off < alen; off += 16) {
+            const uint32_t m = alen - off < 16 ? alen - off : 16;
+            fblock(h, load_partial(ad + off, m), R);
+        }
+    }
+    // steps: the wave's longest record (uniform loop count)
+    const uint32_t steps = wave_max_octet((nch + 7u) >> 3);
+    uint4 m[4];            // the previous block's Poly1305 input (seal: ct; open: the input)
+    bool pend = false;     // m holds a full block whose Horner is not done yet
+    for (uint32_t s = 0; s < steps; ++s) {
+        const uint32_t blk = 8u * s + l;
+        const bool have = blk < nch;
+        const bool full = blk < nfull;
+        // unconditional loads (a lane without a full block reads its slot's
+        // OctetPoly instead): loads under a divergent branch made the compiler
+        // wait for them at the branch's end, before the keystream
+        const uint8_t* src = full ? in + 64u * blk : reinterpret_cast<const uint8_t*>(pwt);
+        uint4 d[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) d[q] = TG_OCTET_NT ? gload16u_nt(src + 16u * q) : gload16u(src + 16u * q);
+        uint32_t ks[16];
+        chacha_block(k, blk + 1u, nv.x, nv.y, nv.z, ks);
+        // the previous block's Horner (ends with the jump over the other
+        // lanes' blocks, or with r when that block was the lane's last)
+        if (pend) {
+            const Mul26& RL = have ? R29 : R;
+            fblock(h, m[0], R);
+            fblock(h, m[1], R);
+            fblock(h, m[2], R);
+            fblock(h, m[3], RL);
+            pend = false;
+        }
+        if (full) {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const uint4 c = make_uint4(d[q].x ^ ks[4 * q], d[q].y ^ ks[4 * q + 1], d[q].z ^ ks[4 * q + 2],
+                                           d[q].w ^ ks[4 * q + 3]);
+                if (TG_OCTET_NT)
+                    gstore16u_nt(out + 64u * blk + 16u * q, c);
+                else
+                    gstore16u(out + 64u * blk + 16u * q, c);
+                m[q] = OPEN ? d[q] : c;
+            }
+            pend = true;
+        } else if (have) {   // the record's partial last block: the lane's last
+            const uint32_t rem = len - 64u * blk;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                if (16u * q < rem) {
+                    const uint32_t mm = rem - 16u * q < 16u ? rem - 16u * q : 16u;
+                    const uint4 dd = load_partial(in + 64u * blk + 16u * q, mm);
+                    const uint4 c = mask_tail(make_uint4(dd.x ^ ks[4 * q], dd.y ^ ks[4 * q + 1], dd.z ^ ks[4 * q + 2],
+                                                         dd.w ^ ks[4 * q + 3]), mm);
+                    store_partial(out + 64u * blk + 16u * q, c, mm);
+                    fblock(h, OPEN ? dd : c, R);
+                }
+            }
+        }
+    }
+    if (pend) {   // the lane's last block was full
+        fblock(h, m[0], R);
+        fblock(h, m[1], R);
+        fblock(h, m[2], R);
+        fblock(h, m[3], R);
+    }
+    // lift and sum over the octet; lane 0 adds the length block
+    const uint32_t nc = (len + 15) >> 4;
+    const uint32_t mlast = nch ? nc - 4u * (nch - 1u) : 0u;
+    h = octet_lift(h, octet_lift_exp(l, nch, mlast), op->r, op->r2, op->r4, op->r8, op->r16);
+    h = octet_sum(h);
+    // le64(len(aad)) || le64(len(ct)) (chacha20_poly1305.py:62-63)
+    fblock(h, make_uint4(alen, 0, len, 0), R);
+    const uint4 tag = octet_finish(h, op->s);
+    const bool tag_aligned = ((((uintptr_t)in | (uintptr_t)out) & 15) == 0) && (len & 15) == 0;
+    if (!valid) return;
+    if (!OPEN) {
+        if (l == 0) store16(out + len, tag, tag_aligned);
+        return;
+    }
+    uint32_t diff = 0;
+    if (l == 0) {
+        const uint4 exp = load16(in + len, tag_aligned);
+        diff = (exp.x ^ tag.x) | (exp.y ^ tag.y) | (exp.z ^ tag.z) | (exp.w ^ tag.w);
+        if (b.status) gst(b.status, i, (uint8_t)(diff == 0));
+    }
+    diff = (uint32_t)__shfl((int)diff, (int)(lane & ~7u), 64);
+    if (diff) {   // chacha20_poly1305.py:90-91: each lane zeroes its own blocks
+        const uint4 z = make_uint4(0, 0, 0, 0);
+        for (uint32_t blk = l; blk < nch; blk += 8) {
+            const uint32_t rem = len - 64u * blk;
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+                if (16u * q < rem) store_partial(out + 64u * blk + 16u * q, z, rem - 16u * q < 16u ? rem - 16u * q : 16u);
+        }
+    }
+}
+
 // Up to this many records a batch runs one record per wavefront (see the
 // GCM launcher; at 16 KiB the kernels meet between 2^15 and 2^16 records:
 // profiles/r01/v21_smallbatch.txt).
@@ -626,10 +809,31 @@ bool wave_path(uint64_t n) {
     return v == 3 || (v == 0 && n <= kWaveMaxRecords);
 }
 
+// The octet kernel (single key): the one-time keys and powers of r into
+// per-launch scratch (api.hip stream_alloc), then the records.
+template <bool OPEN>
+int launch_octet(const ChachaKeyDev* key, const tg_batch& b, hipStream_t s, const uint32_t* order) {
+    const uint64_t groups = (b.n + (kOctetThreads / 8) - 1) / (kOctetThreads / 8);
+    if (groups > 0x7fffffffull) return TG_EINVAL;
+    OctetPoly* pw = nullptr;
+    if (stream_alloc((void**)&pw, sizeof(OctetPoly) * b.n, s)) return TG_EHIP;
+    hipLaunchKernelGGL(chacha_otk_kernel, dim3((unsigned)((b.n + 255) / 256)), dim3(256), 0, s, key, b, order, pw);
+    int rc = hipGetLastError() == hipSuccess ? TG_OK : TG_EHIP;
+    if (!rc) {
+        hipLaunchKernelGGL((chacha_octet_kernel<OPEN>), dim3((unsigned)groups), dim3(kOctetThreads), 0, s, key, b,
+                           order, pw);
+        rc = hipGetLastError() == hipSuccess ? TG_OK : TG_EHIP;
+    }
+    if (stream_free(pw, s) && !rc) rc = TG_EHIP;
+    return rc;
+}
+
 template <bool OPEN, bool MULTIKEY>
 int launch(const ChachaKeyDev* keys, uint64_t nkeys, const tg_batch& b, hipStream_t s, const uint32_t* order) {
     const int v = opt(kOptChachaVariant);
-    if (v != 0 && v != 3 && v != 4 && v != 5) return TG_EINVAL;
+    if (v != 0 && v != 3 && v != 4 && v != 5 && v != 6) return TG_EINVAL;
+    // 6: the octet kernel for every single-key batch (key tables: the lane kernel)
+    if (v == 6 && !MULTIKEY) return launch_octet<OPEN>(keys, b, s, order);
     if (wave_path(b.n)) {
         // waves per record as in the GCM launcher (aes_gcm.hip waves_per_record)
         const int o = opt(kOptWavesPerRecord);

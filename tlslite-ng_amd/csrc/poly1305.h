@@ -277,5 +277,112 @@ __device__ __forceinline__ F5 stripe_sum(F5 z, F5* s_part, uint32_t seg, uint32_
     return z;
 }
 
+// ---- octet striping (chacha_octet_kernel, selftest mode 4) ----------------
+// Eight lanes per message; lane l owns the 64-byte chunks b = l, l + 8, ...
+// (ChaCha blocks b of the record), i.e. the Poly1305 blocks 4 b .. 4 b + 3.
+// Its Horner multiplies by r within a chunk and by r^29 after a chunk's last
+// block (the other seven lanes' 28 blocks lie between), and by r after its
+// own last block; its value is then lifted by r^f (octet_lift_exp) and the
+// eight partials are summed over the octet.  All in 26-bit limbs: r^29 and
+// the lift powers are general 130-bit values, which the radix-2^32 clamp
+// trick (Poly32) cannot multiply by.
+
+// A multiplier in 26-bit limbs with 5 x limbs 1..4 (2^130 == 5).
+struct Mul26 {
+    uint32_t r0, r1, r2, r3, r4, s1, s2, s3, s4;
+};
+
+__device__ __forceinline__ Mul26 mul26(const F5& r) {
+    return Mul26{r.h0, r.h1, r.h2, r.h3, r.h4, r.h1 * 5, r.h2 * 5, r.h3 * 5, r.h4 * 5};
+}
+
+// h = (h + LE(m) + hib 2^128) * R mod 2^130 - 5 (poly1305.py:43-46 with any
+// multiplier): poly_block with R instead of the key's r.
+__device__ __forceinline__ void fblock(F5& h, uint4 m, const Mul26& R, uint32_t hib = 1u << 24) {
+    const uint32_t M26 = 0x3ffffffu;
+    uint32_t h0 = h.h0 + (m.x & M26);
+    uint32_t h1 = h.h1 + (__builtin_amdgcn_alignbit(m.y, m.x, 26) & M26);
+    uint32_t h2 = h.h2 + (__builtin_amdgcn_alignbit(m.z, m.y, 20) & M26);
+    uint32_t h3 = h.h3 + (__builtin_amdgcn_alignbit(m.w, m.z, 14) & M26);
+    uint32_t h4 = h.h4 + ((m.w >> 8) | hib);
+    uint64_t d0 = mul64(h0, R.r0) + mul64(h1, R.s4) + mul64(h2, R.s3) + mul64(h3, R.s2) + mul64(h4, R.s1);
+    uint64_t d1 = mul64(h0, R.r1) + mul64(h1, R.r0) + mul64(h2, R.s4) + mul64(h3, R.s3) + mul64(h4, R.s2);
+    uint64_t d2 = mul64(h0, R.r2) + mul64(h1, R.r1) + mul64(h2, R.r0) + mul64(h3, R.s4) + mul64(h4, R.s3);
+    uint64_t d3 = mul64(h0, R.r3) + mul64(h1, R.r2) + mul64(h2, R.r1) + mul64(h3, R.r0) + mul64(h4, R.s4);
+    uint64_t d4 = mul64(h0, R.r4) + mul64(h1, R.r3) + mul64(h2, R.r2) + mul64(h3, R.r1) + mul64(h4, R.r0);
+    uint32_t c;
+    c = (uint32_t)(d0 >> 26); h0 = (uint32_t)d0 & M26;
+    d1 += c; c = (uint32_t)(d1 >> 26); h1 = (uint32_t)d1 & M26;
+    d2 += c; c = (uint32_t)(d2 >> 26); h2 = (uint32_t)d2 & M26;
+    d3 += c; c = (uint32_t)(d3 >> 26); h3 = (uint32_t)d3 & M26;
+    d4 += c; c = (uint32_t)(d4 >> 26); h4 = (uint32_t)d4 & M26;
+    h0 += c * 5; c = h0 >> 26; h0 &= M26;
+    h1 += c;
+    h.h0 = h0; h.h1 = h1; h.h2 = h2; h.h3 = h3; h.h4 = h4;
+}
+
+// The per-message powers of r the octet lanes use: r (F5), r^2, r^4, r^8,
+// r^16 (the lift), r^29 (the jump), and s.  36 words (144 bytes) per
+// message, written by chacha_otk_kernel (the one-time key, block 0).
+struct OctetPoly {
+    uint32_t r[5], r2[5], r4[5], r8[5], r16[5], r29[5];
+    uint32_t s[4];
+    uint32_t pad[2];
+};
+static_assert(sizeof(OctetPoly) == 144, "OctetPoly layout");
+
+__device__ __forceinline__ F5 f5_at(const uint32_t* w) { return F5{w[0], w[1], w[2], w[3], w[4]}; }
+
+// The powers from the clamped r (poly1305.py:37-38) in 26-bit limbs.
+__device__ __forceinline__ void octet_powers(const F5& r, OctetPoly& o) {
+    const F5 r2 = fmul(r, r), r4 = fmul(r2, r2), r8 = fmul(r4, r4), r16 = fmul(r8, r8);
+    const F5 r29 = fmul(fmul(fmul(r16, r8), r4), r);
+    const F5* src[6] = {&r, &r2, &r4, &r8, &r16, &r29};
+    uint32_t* dst[6] = {o.r, o.r2, o.r4, o.r8, o.r16, o.r29};
+#pragma unroll
+    for (int k = 0; k < 6; ++k) {
+        dst[k][0] = src[k]->h0; dst[k][1] = src[k]->h1; dst[k][2] = src[k]->h2;
+        dst[k][3] = src[k]->h3; dst[k][4] = src[k]->h4;
+    }
+}
+
+// The lift exponent of an octet lane: lanes own 64-byte chunks b = l mod 8;
+// nch chunks in all (the last holding mlast Poly1305 blocks, 1..4).  The lane
+// whose chunk is the last (b_last = nch - 1) needs nothing more (0); the
+// lane d chunks before it (d = 1..7) had its Horner end d chunks early and
+// needs r^(4 (d - 1) + mlast).  Lanes without a chunk return 0 (their value
+// is zero, whatever the lift).
+__device__ __forceinline__ uint32_t octet_lift_exp(uint32_t l, uint32_t nch, uint32_t mlast) {
+    if (nch == 0 || l >= nch) return 0;
+    const uint32_t d = (nch - 1u - l) & 7u;
+    return d ? 4u * (d - 1u) + mlast : 0u;
+}
+
+// v * r^f for f < 32 from the stored powers (one multiply per set bit).
+__device__ __forceinline__ F5 octet_lift(F5 v, uint32_t f, const uint32_t* r, const uint32_t* r2,
+                                         const uint32_t* r4, const uint32_t* r8, const uint32_t* r16) {
+    if (f & 1u) v = fmul(v, f5_at(r));
+    if (f & 2u) v = fmul(v, f5_at(r2));
+    if (f & 4u) v = fmul(v, f5_at(r4));
+    if (f & 8u) v = fmul(v, f5_at(r8));
+    if (f & 16u) v = fmul(v, f5_at(r16));
+    return v;
+}
+
+// Sum of the eight partials of an octet (lanes 8 q .. 8 q + 7).
+__device__ __forceinline__ F5 octet_sum(F5 z) {
+#pragma unroll
+    for (int m = 1; m < 8; m <<= 1) z = fnorm_add(z, fshfl_xor(z, m));
+    return z;
+}
+
+// tag = LE16((acc + s) mod 2^128) for an F5 accumulator (poly1305.py:47-48).
+__device__ __forceinline__ uint4 octet_finish(const F5& h, const uint32_t* s) {
+    Poly p;
+    p.h0 = h.h0; p.h1 = h.h1; p.h2 = h.h2; p.h3 = h.h3; p.h4 = h.h4;
+    p.p0 = s[0]; p.p1 = s[1]; p.p2 = s[2]; p.p3 = s[3];
+    return poly_finish(p);
+}
+
 }  // namespace
 }  // namespace tg

@@ -9,7 +9,10 @@
 //   0  lane Horner in radix 2^32 (Poly32), as chacha_kernel (one message per lane);
 //   1  wave-striped Horner with the r^(4S-4) gaps, the lift and the shuffle
 //      sum of chacha_wave_kernel, W = 1 (S = 64 threads per message);
-//   2  the same with W = 4;  3  W = 16.
+//   2  the same with W = 4;  3  W = 16;
+//   4  the octet striping of chacha_octet_kernel: eight lanes per message,
+//      lane l the 64-byte chunks l, l + 8, ..., r within a chunk and r^29
+//      across the other lanes' chunks, the lift and the octet sum.
 // GHASH modes (ghash.h):
 //   0  Horner with gmul (8-bit tables, j * 4096 + b * 16: the T-table lane
 //      kernel and the wave kernel);  1  gmul_lowreg;
@@ -115,6 +118,44 @@ __global__ __launch_bounds__(64 * W) void poly_wave_kernel(const uint8_t* keys, 
     p.h0 = z.h0; p.h1 = z.h1; p.h2 = z.h2; p.h3 = z.h3; p.h4 = z.h4;
     const uint4 tag = poly_finish(p);
     if (seg == 0) store_partial(tags + 16 * i, tag, 16);
+}
+
+// Eight messages per 64-thread workgroup, one octet each (mode 4).
+__global__ __launch_bounds__(64) void poly_octet_kernel(const uint8_t* keys, const uint8_t* msgs,
+                                                        const uint64_t* off, const uint32_t* len, uint64_t n,
+                                                        uint8_t* tags) {
+    const uint32_t l = threadIdx.x & 7u;
+    const uint64_t i = (uint64_t)blockIdx.x * 8 + (threadIdx.x >> 3);
+    const bool valid = i < n;
+    uint32_t otk[16] = {0};
+    const uint64_t ik = valid ? i : 0;
+    const uint4 k0 = load_partial(keys + 32 * ik, 16), k1 = load_partial(keys + 32 * ik + 16, 16);
+    otk[0] = k0.x; otk[1] = k0.y; otk[2] = k0.z; otk[3] = k0.w;
+    otk[4] = k1.x; otk[5] = k1.y; otk[6] = k1.z; otk[7] = k1.w;
+    Poly p;
+    poly_init(p, otk);
+    OctetPoly o;   // as chacha_otk_kernel
+    octet_powers(F5{p.r0, p.r1, p.r2, p.r3, p.r4}, o);
+    const Mul26 R = mul26(f5_at(o.r)), R29 = mul26(f5_at(o.r29));
+    const uint8_t* m = msgs + (valid ? off[i] : 0);
+    const uint32_t nbytes = valid ? len[i] : 0, nb = (nbytes + 15) >> 4, nch = (nb + 3) >> 2;
+    F5 h = {0, 0, 0, 0, 0};
+    for (uint32_t c = l; c < nch; c += 8) {   // the lane's chunks, as chacha_octet_kernel's blocks
+        const bool last = c + 8 >= nch;
+#pragma unroll
+        for (uint32_t q = 0; q < 4; ++q) {
+            const uint32_t k = 4 * c + q;
+            if (k >= nb) break;
+            uint32_t hib;
+            const uint4 blk = msg_block(m, nbytes, k, true, hib);
+            fblock(h, blk, (q == 3 && !last) ? R29 : R, hib);
+        }
+    }
+    const uint32_t mlast = nch ? nb - 4u * (nch - 1u) : 0u;
+    h = octet_lift(h, octet_lift_exp(l, nch, mlast), o.r, o.r2, o.r4, o.r8, o.r16);
+    h = octet_sum(h);
+    const uint4 tag = octet_finish(h, (const uint32_t[4]){p.p0, p.p1, p.p2, p.p3});
+    if (valid && l == 0) store_partial(tags + 16 * i, tag, 16);
 }
 
 // ---- GHASH ----------------------------------------------------------------
@@ -243,7 +284,7 @@ size_t span(const uint64_t* off, const uint32_t* len, uint64_t n) {
 extern "C" __attribute__((visibility("default"))) int tg_selftest_poly1305(
     int mode, const uint8_t* keys, const uint8_t* msgs, const uint64_t* off, const uint32_t* len,
     uint64_t n, uint8_t* tags) {
-    if (!keys || !off || !len || !tags || mode < 0 || mode > 3 || n == 0 || n > (1u << 20))
+    if (!keys || !off || !len || !tags || mode < 0 || mode > 4 || n == 0 || n > (1u << 20))
         return TG_EINVAL;
     DevBufs d;
     const size_t ms = span(off, len, n);
@@ -260,8 +301,11 @@ extern "C" __attribute__((visibility("default"))) int tg_selftest_poly1305(
         hipLaunchKernelGGL(tg::poly_wave_kernel<1>, dim3((unsigned)n), dim3(64), 0, 0, dk, dm, doff, dlen, dt);
     else if (mode == 2)
         hipLaunchKernelGGL(tg::poly_wave_kernel<4>, dim3((unsigned)n), dim3(256), 0, 0, dk, dm, doff, dlen, dt);
-    else
+    else if (mode == 3)
         hipLaunchKernelGGL(tg::poly_wave_kernel<16>, dim3((unsigned)n), dim3(1024), 0, 0, dk, dm, doff, dlen, dt);
+    else
+        hipLaunchKernelGGL(tg::poly_octet_kernel, dim3((unsigned)((n + 7) / 8)), dim3(64), 0, 0, dk, dm, doff, dlen,
+                           n, dt);
     if (hipGetLastError() != hipSuccess || hipDeviceSynchronize() != hipSuccess) return TG_EHIP;
     return hipMemcpy(tags, dt, 16 * n, hipMemcpyDeviceToHost) == hipSuccess ? TG_OK : TG_EHIP;
 }

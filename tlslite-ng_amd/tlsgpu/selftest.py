@@ -11,7 +11,8 @@ import numpy as np
 from . import _lib
 
 POLY_MODES = {0: "lane Horner (batch kernel)", 1: "wave-striped, 1 wave",
-              2: "wave-striped, 4 waves", 3: "wave-striped, 16 waves"}
+              2: "wave-striped, 4 waves", 3: "wave-striped, 16 waves",
+              4: "octet-striped, 8 lanes (octet kernel)"}
 GHASH_MODES = {0: "8-bit tables", 1: "8-bit tables, 8 rows in flight", 2: "rotated tables",
                3: "table-free clmul", 4: "octet H^8 stride + lift", 5: "wave H^64 stride + lift",
                6: "octet H^8 stride, 4-bit wave tables (key-table octet kernel)"}
