@@ -47,13 +47,16 @@ def test_many_streams_memory_flat(oracle_mod):
     assert bufs1 <= bufs0 + 1 and bytes1 <= bytes0 + (2 << 20), (bytes0, bufs0, bytes1, bufs1)
     # Device memory as a whole: the first launch of a kernel with a private
     # segment (the hybrid AES-GCM kernel spills 22 VGPRs, 92 B per lane) on a
-    # fresh queue makes the HIP runtime allocate that queue's scratch, 3.0 MiB
-    # measured; kernels without one (tg_make_nonces, a torch elementwise op)
-    # add 0 (tools/stream_mem_probe.py, profiles/r06/x1/stream_mem.jsonl).
-    # So the growth is bounded by 3 MiB per distinct stream (torch's pool has
-    # 32), plus the library's own scratch checked above, plus slack.
+    # fresh queue makes the HIP runtime allocate that queue's scratch.
+    # tools/stream_mem_probe.py (profiles/r06/x10/stream_mem.jsonl) measured,
+    # per stream, on raw HIP streams 3.0 MiB for such a kernel and 0 for one
+    # without (tg_make_nonces, a torch elementwise op), and on torch's pool
+    # streams 5.7 MiB for the AES-GCM batch against 1.2 MiB for tg_make_nonces
+    # (the pool's streams are set up on first use).  So the growth is bounded
+    # by 6 MiB per distinct stream (the pool has 32), plus the library's own
+    # scratch checked above, plus slack.
     grew = free0 - free1
-    bound = 32 * (3 << 20) + (bytes1 - bytes0) + (8 << 20)
+    bound = 32 * (6 << 20) + (bytes1 - bytes0) + (8 << 20)
     assert grew <= bound, (grew / 2**20, bound / 2**20)
     # many launches in flight on one stream reuse one buffer (stream order)
     for _ in range(20):

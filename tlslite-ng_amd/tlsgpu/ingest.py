@@ -120,27 +120,47 @@ class _Slot(object):
         self.d_data = torch.empty(nrec * data_stride, dtype=u8, device="cuda")
         self.d_wire = torch.empty(nrec * wire_stride + 16, dtype=u8, device="cuda")
         self.d_pack = torch.empty(nrec * wire_stride, dtype=u8, device="cuda")
-        # per-record metadata: host staging (pinned) and device copies
-        self.h_len = torch.empty(nrec, dtype=torch.int32).pin_memory()
-        self.h_ctype = torch.empty(nrec, dtype=u8).pin_memory()
-        self.h_pack = torch.empty(nrec, dtype=torch.int64).pin_memory()
-        self.h_status = torch.empty(nrec, dtype=u8).pin_memory()
-        self.d_len = torch.empty(nrec, dtype=torch.int32, device="cuda")
-        self.d_wlen = torch.empty(nrec, dtype=torch.int32, device="cuda")
-        self.d_ctype = torch.empty(nrec, dtype=u8, device="cuda")
-        self.d_pack_off = torch.empty(nrec, dtype=torch.int64, device="cuda")
-        self.d_status = torch.empty(nrec, dtype=u8, device="cuda")
+        # per-record metadata: one pinned host block and one device block with
+        # the same layout, so each direction moves it in ONE copy per batch
+        # (small copies run as blit kernels at ~5 us each, plus the host's
+        # launch overhead):
+        #   P int64 @0     pack offsets          S int64 @8n   writer app / reader wire offsets
+        #   L int32 @16n   lengths               R int32 @20n  reader wire lengths / writer wire lengths
+        #   Q int32 @24n   reader packed lengths T u8 @28n     content types     U u8 @29n  status
+        self.nrec = nrec
+        self.h_meta = torch.empty(32 * nrec, dtype=u8).pin_memory()
+        self.d_meta = torch.empty(32 * nrec, dtype=u8, device="cuda")
+
+        def views(m):
+            n = nrec
+            return (m[0:8 * n].view(torch.int64), m[8 * n:16 * n].view(torch.int64),
+                    m[16 * n:20 * n].view(torch.int32), m[20 * n:24 * n].view(torch.int32),
+                    m[24 * n:28 * n].view(torch.int32), m[28 * n:29 * n], m[29 * n:30 * n])
+        (self.h_pack, self.h_src, self.h_len, self.h_rl, self.h_plen, self.h_ctype,
+         self.h_status) = views(self.h_meta)
+        (self.d_pack_off, self.d_src, self.d_len, self.d_wlen, self.d_plen, self.d_ctype,
+         self.d_status) = views(self.d_meta)
+        self.d_rl = self.d_wlen
+        self.h_app_off, self.d_app_off = self.h_src, self.d_src
         idx = torch.arange(nrec, dtype=torch.int64, device="cuda")
         self.d_data_off = idx * data_stride
         self.d_wire_off = idx * wire_stride + wire_lead
         if app_bytes:   # the writer's application data, contiguous
             self.h_app = torch.empty(app_bytes, dtype=u8).pin_memory()
             self.d_app = torch.empty(app_bytes, dtype=u8, device="cuda")
-            self.h_app_off = torch.empty(nrec, dtype=torch.int64).pin_memory()
-            self.d_app_off = torch.empty(nrec, dtype=torch.int64, device="cuda")
         self.n = 0
         self.nbytes = 0
         self.app = 0
+
+    # metadata rows in units of nrec bytes: P [0, 8), S [8, 16), L [16, 20),
+    # R [20, 24), Q [24, 28), T [28, 29), U [29, 30)
+    def meta_to_device(self, lo, hi):
+        n = self.nrec
+        self.d_meta[lo * n:hi * n].copy_(self.h_meta[lo * n:hi * n], non_blocking=True)
+
+    def meta_to_host(self, lo, hi):
+        n = self.nrec
+        self.h_meta[lo * n:hi * n].copy_(self.d_meta[lo * n:hi * n], non_blocking=True)
 
 
 class RecordWriter(object):
@@ -285,10 +305,7 @@ class RecordWriter(object):
         with torch.cuda.stream(s.stream):
             if s.app:
                 s.d_app[:s.app].copy_(s.h_app[:s.app], non_blocking=True)
-            s.d_len[:n].copy_(s.h_len[:n], non_blocking=True)
-            s.d_ctype[:n].copy_(s.h_ctype[:n], non_blocking=True)
-            s.d_pack_off[:n].copy_(s.h_pack[:n], non_blocking=True)
-            s.d_app_off[:n].copy_(s.h_app_off[:n], non_blocking=True)
+            s.meta_to_device(0, 29)        # pack and app offsets, lengths, types (R: seal's output)
             s.app_event.record(s.stream)   # h_app and the row metadata may be refilled
             # the fragments into their aligned rows (room for the inner type,
             # padding and tag after each)
@@ -352,21 +369,10 @@ class RecordReader(object):
         self.slot = _Slot(torch, self.batch, self.data_stride, self.wire_stride, self.lead)
         self.h_off = np.empty(self.batch, np.uint64)
         self.h_rlen = np.empty(self.batch, np.uint32)
-        self.h_plen = torch.empty(self.batch, dtype=torch.int32).pin_memory()
-        self.h_src = torch.empty(self.batch, dtype=torch.int64).pin_memory()
-        self.h_rl = torch.empty(self.batch, dtype=torch.int32).pin_memory()
-        self.d_src = torch.empty(self.batch, dtype=torch.int64, device="cuda")
-        self.d_rl = torch.empty(self.batch, dtype=torch.int32, device="cuda")
         self.h_out = torch.empty(self.batch * self.data_stride, dtype=torch.uint8).pin_memory()
         # the pipelined bulk path (read_application_data): per-slot gather indices
         self.rslots = [self.slot] + [_Slot(torch, self.batch, self.data_stride, self.wire_stride,
                                            self.lead) for _ in range(max(1, nslots) - 1)]
-        for s in self.rslots:
-            s.h_src = torch.empty(self.batch, dtype=torch.int64).pin_memory()
-            s.h_rl = torch.empty(self.batch, dtype=torch.int32).pin_memory()
-            s.h_plen = torch.empty(self.batch, dtype=torch.int32).pin_memory()
-            s.d_src = torch.empty(self.batch, dtype=torch.int64, device="cuda")
-            s.d_rl = torch.empty(self.batch, dtype=torch.int32, device="cuda")
         self.pending_error = None
         self._pool = None
 
@@ -564,15 +570,12 @@ class RecordReader(object):
         self.seq += n
         with torch.cuda.stream(s.stream):
             s.d_pack[:used].copy_(self.h_buf[start:start + used], non_blocking=True)
-            s.d_src[:n].copy_(s.h_src[:n], non_blocking=True)
-            s.d_rl[:n].copy_(s.h_rl[:n], non_blocking=True)
+            s.meta_to_device(8, 24)        # wire offsets and lengths (L: open's output)
             gather(s.d_pack, s.d_src, s.d_rl, s.d_wire, s.d_wire_off, n, stream=s.stream)
             open_records(self.key, self.version, self.fixed_iv, s.seq, n, s.d_wire,
                          s.d_wire_off, s.d_rl, s.d_data, s.d_data_off, s.d_len, s.d_ctype,
                          s.d_status, stream=s.stream, recv_limit=self.recv_record_limit)
-            s.h_len[:n].copy_(s.d_len[:n], non_blocking=True)
-            s.h_ctype[:n].copy_(s.d_ctype[:n], non_blocking=True)
-            s.h_status[:n].copy_(s.d_status[:n], non_blocking=True)
+            s.meta_to_host(16, 30)         # lengths, types, status (R and Q come back unchanged)
             s.event.record(s.stream)
 
     def _pack(self, s, dst, direct, pieces):
@@ -615,9 +618,8 @@ class RecordReader(object):
             pieces.append(piece)
             s.target = piece
         with torch.cuda.stream(s.stream):
-            s.d_pack_off[:k].copy_(s.h_pack[:k], non_blocking=True)
-            s.d_wlen[:k].copy_(s.h_plen[:k], non_blocking=True)
-            gather(s.d_data, s.d_data_off, s.d_wlen, s.d_pack, s.d_pack_off, k, stream=s.stream)
+            s.meta_to_device(0, 28)        # pack offsets and packed lengths (S, L, R as uploaded / read)
+            gather(s.d_data, s.d_data_off, s.d_plen, s.d_pack, s.d_pack_off, k, stream=s.stream)
             if isinstance(s.target, bytearray):
                 tgt = np.frombuffer(s.target, np.uint8)
             else:
@@ -670,21 +672,17 @@ class RecordReader(object):
         records before the first failing one (whose error is kept pending)."""
         torch = self.torch
         s = self.slot
-        src = self.h_src.numpy()
-        src[:n] = self.h_off[:n].astype(np.int64)
-        self.h_rl.numpy()[:n] = self.h_rlen[:n].astype(np.int32)
+        s.h_src.numpy()[:n] = self.h_off[:n].astype(np.int64)
+        s.h_rl.numpy()[:n] = self.h_rlen[:n].astype(np.int32)
         with torch.cuda.stream(s.stream):
             s.d_pack[:used].copy_(self.h_buf[:used], non_blocking=True)
-            self.d_src[:n].copy_(self.h_src[:n], non_blocking=True)
-            self.d_rl[:n].copy_(self.h_rl[:n], non_blocking=True)
+            s.meta_to_device(8, 24)
             # wire records into 16-byte aligned slots (payload after header aligned)
-            gather(s.d_pack, self.d_src, self.d_rl, s.d_wire, s.d_wire_off, n, stream=s.stream)
+            gather(s.d_pack, s.d_src, s.d_rl, s.d_wire, s.d_wire_off, n, stream=s.stream)
             open_records(self.key, self.version, self.fixed_iv, self.seq, n, s.d_wire,
-                         s.d_wire_off, self.d_rl, s.d_data, s.d_data_off, s.d_len, s.d_ctype,
+                         s.d_wire_off, s.d_rl, s.d_data, s.d_data_off, s.d_len, s.d_ctype,
                          s.d_status, stream=s.stream, recv_limit=self.recv_record_limit)
-            self.h_plen[:n].copy_(s.d_len[:n], non_blocking=True)
-            s.h_ctype[:n].copy_(s.d_ctype[:n], non_blocking=True)
-            s.h_status[:n].copy_(s.d_status[:n], non_blocking=True)
+            s.meta_to_host(16, 30)
             s.event.record(s.stream)
         s.event.synchronize()
         # the unconsumed tail to the front (the copy above has read h_buf)
@@ -694,7 +692,7 @@ class RecordReader(object):
             buf[:tail] = buf[used:self.fill].copy()
         self.fill = tail
         st = s.h_status.numpy()[:n]
-        plen = self.h_plen.numpy()[:n]
+        plen = s.h_len.numpy()[:n]
         ct = s.h_ctype.numpy()[:n]
         bad = np.nonzero(st)[0]
         k = int(bad[0]) if len(bad) else n

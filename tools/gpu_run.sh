@@ -85,7 +85,8 @@ for st0 in "$@"; do
     pmcroles)
       bash tools/pmc_roles2.sh $T/pmc_roles ;;
     memprobe)   # device memory per fresh stream by launch kind (tools/stream_mem_probe.py)
-      timeout -k 10 300 python -u tools/stream_mem_probe.py > $O/stream_mem.jsonl 2> $O/stream_mem.err; cat $O/stream_mem.jsonl ;;
+      timeout -k 10 300 python -u tools/stream_mem_probe.py > $O/stream_mem.jsonl 2> $O/stream_mem.err
+      timeout -k 10 600 python -u tools/stream_mem_probe.py --torch-pool >> $O/stream_mem.jsonl 2>> $O/stream_mem.err; cat $O/stream_mem.jsonl ;;
     c4fetch)
       for c in FETCH_SIZE WRITE_SIZE; do
         (cd /tmp && export TMPDIR=/tmp && timeout -k 10 240 rocprofv3 --pmc $c --kernel-trace --output-format csv \

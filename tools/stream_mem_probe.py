@@ -81,5 +81,40 @@ def main():
                           "other_per_stream_mib": round(used / 24 / 2**20, 3)}), flush=True)
 
 
+def torch_pool(kinds):
+    """The same on torch's own stream pool (32 streams per device, created
+    together on first use, handed out round robin), as tests/test_gpu_scratch.py
+    uses: a separate process per kind, so every kind meets fresh pool streams."""
+    import subprocess
+    for name in kinds:
+        code = (
+            "import sys, json; sys.path[:0] = %r\n"
+            "import torch, tlsgpu\n"
+            "from vectors import tls13_aad\n"
+            "n, L = 65536, 1024\n"
+            "inp = torch.randint(0, 256, (n * L,), dtype=torch.uint8, device='cuda')\n"
+            "out = torch.zeros(n * (L + 16), dtype=torch.uint8, device='cuda')\n"
+            "nonces = torch.zeros(12 * n, dtype=torch.uint8, device='cuda')\n"
+            "aad = torch.tensor(list(tls13_aad(L)), dtype=torch.uint8, device='cuda')\n"
+            "b = tlsgpu.make_batch(n, inp, out, nonces, aad=aad, fixed_len=L, in_stride=L, out_stride=L + 16, fixed_aad_len=5)\n"
+            "gcm = tlsgpu.HipAESGCM(bytearray(16))\n"
+            "f = {'nonces': lambda st: tlsgpu.make_nonces(bytes(12), 0, n, nonces, stream=st),"
+            " 'aesgcm': lambda st: tlsgpu.seal_batch(gcm, b, st)}[%r]\n"
+            "f(None); torch.cuda.synchronize()\n"
+            "streams = [torch.cuda.Stream() for _ in range(40)]\n"
+            "torch.cuda.synchronize(); free0 = torch.cuda.mem_get_info()[0]; lib0 = tlsgpu.scratch_info()[0]\n"
+            "for st in streams:\n"
+            "    f(st); st.synchronize()\n"
+            "torch.cuda.synchronize(); free1 = torch.cuda.mem_get_info()[0]; lib1 = tlsgpu.scratch_info()[0]\n"
+            "print(json.dumps({'kind': 'torch_pool_' + %r, 'streams': 40, 'device_bytes': free0 - free1,"
+            " 'library_scratch_bytes': lib1 - lib0, 'per_pool_stream_mib': round((free0 - free1 - (lib1 - lib0)) / 32 / 2**20, 3)}))\n"
+        ) % ([ROOT, os.path.join(ROOT, "tlslite-ng_amd"), os.path.join(ROOT, "tests", "golden")], name, name)
+        r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=240)
+        print(r.stdout.strip() or r.stderr[-500:], flush=True)
+
+
 if __name__ == "__main__":
+    if "--torch-pool" in sys.argv:
+        torch_pool(["nonces", "aesgcm"])
+        sys.exit(0)
     main()
