@@ -540,8 +540,8 @@ int lds_attr(const void* fn, int bytes) {
 // list of device buffers, each free for reuse once the event recorded behind
 // its last launch has completed.  A buffer released on a stream is taken
 // again at once only by the next launch on that same stream handle -- never
-// through hipStreamPerThread or the null stream, whose handle names a
-// different stream in each thread -- and that launch's stream also waits for
+// through hipStreamPerThread, whose handle names a different stream in each
+// thread -- and that launch's stream also waits for
 // the buffer's event, so a handle that a destroyed stream left behind and a
 // new stream took over cannot reuse a buffer whose work is still pending
 // (on the stream that recorded the event the wait orders
@@ -565,7 +565,14 @@ std::vector<ScratchBuf>& scratch_list() {
     static std::vector<ScratchBuf>* v = new std::vector<ScratchBuf>();   // outlives static teardown
     return *v;
 }
-bool per_thread_handle(hipStream_t s) { return s == nullptr || s == hipStreamPerThread; }
+// hipStreamPerThread names a different stream in each thread.  The null
+// stream does not: this library is built without per-thread default
+// streams, so 0 is the device's legacy default stream, one per device (and
+// buffers and helpers are kept per device).  Round 6 treated 0 as
+// per-thread too: every key-table batch on the default stream then created a
+// new helper stream while the last one's work was in flight (config 4
+// 657 -> 547 GiB/s, profiles/r06/f2/bench_c4.json).
+bool per_thread_handle(hipStream_t s) { return s == hipStreamPerThread; }
 constexpr size_t kScratchHigh = (size_t)8 << 30;
 
 // Frees idle buffers whose last launch has completed until the cache holds

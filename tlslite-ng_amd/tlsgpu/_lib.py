@@ -140,12 +140,17 @@ def load():
     l.tg_set_option.argtypes = [ctypes.c_char_p, i]
     l.tg_get_option.argtypes = [ctypes.c_char_p, ctypes.POINTER(ctypes.c_int)]
     l.tg_scratch_info.argtypes = [ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64)]
-    l.tg_scratch_trim.argtypes = [ctypes.c_uint64]
-    l.tg_host_copy.argtypes = [p, p, sz, i]
-    l.tg_host_copy_rows.argtypes = [p, sz, p, sz, sz, sz, i]
-    l.tg_helper_info.argtypes = [ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64)]
+    # round-6 entry points; an older build under TLSGPU_LIB (A/B timing of a
+    # previous round's library) has none of them and loads without
+    if os.environ.get("TLSGPU_LIB") is None or hasattr(l, "tg_host_copy"):
+        l.tg_scratch_trim.argtypes = [ctypes.c_uint64]
+        l.tg_host_copy.argtypes = [p, p, sz, i]
+        l.tg_host_copy_rows.argtypes = [p, sz, p, sz, sz, sz, i]
+        l.tg_helper_info.argtypes = [ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64)]
     for name in EXPORTS:
         if name not in ("tg_version", "tg_last_error"):
+            if os.environ.get("TLSGPU_LIB") is not None and not hasattr(l, name):
+                continue   # an older build under TLSGPU_LIB (A/B timing)
             getattr(l, name).restype = ctypes.c_int
     l.tg_scan_records.restype = ctypes.c_int64
     ver = l.tg_version().decode()
