@@ -299,7 +299,7 @@ def main():
                     help="CPU baseline: seconds each process seals/opens")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--e2e", action="store_true", help="also time the host<->device path")
-    ap.add_argument("--traffic-file", default=os.path.join(ROOT, "profiles", "r05", "traffic.json"),
+    ap.add_argument("--traffic-file", default=os.path.join(ROOT, "profiles", "r06", "traffic.json"),
                     help="per-launch HBM bytes from tools/traffic.sh (rocprofv3 FETCH_SIZE / "
                          "WRITE_SIZE passes at this config, calibrated per access shape) for "
                          "roofline.traffic")
