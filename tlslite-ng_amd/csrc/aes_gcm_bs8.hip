@@ -209,10 +209,11 @@ struct SingleKeyRowCtx {
     const GcmKeyDev* key;
     uint4 jw;
     const uint4* mt = nullptr;   // per slot E_K(J0) (hy_mask_kernel), or computed per record
+    uint32_t tid = threadIdx.x;  // (gcm_hy_kernel passes it through an empty asm per job)
     __device__ __forceinline__ const uint32_t* rk() const { return key->rk; }
     __device__ __forceinline__ uint4 hpow(int e) const { return key->hpow[e - 1]; }
-    __device__ __forceinline__ uint4 gmul(uint4 y) const { return gmul_rot_j(y, threadIdx.x & 15u, jw); }
-    __device__ __forceinline__ uint4 gmulx(uint4 y, uint4 x) const { return gmul_rot_j(y, threadIdx.x & 15u, jw, x); }
+    __device__ __forceinline__ uint4 gmul(uint4 y) const { return gmul_rot_j(y, tid & 15u, jw); }
+    __device__ __forceinline__ uint4 gmulx(uint4 y, uint4 x) const { return gmul_rot_j(y, tid & 15u, jw, x); }
     __device__ __forceinline__ const uint4* masks() const { return mt; }
 };
 struct TableKeyCtx {    // a key of a key table: the wave's 4-bit H^8 tables in LDS (gmul4)
@@ -251,7 +252,7 @@ template <int NR, bool OPEN, bool TROLE, class KM, class KC, bool PRE = false, i
 __device__ __forceinline__ void octet_job(const KC& kc, const tg_batch& b,
                                           const uint32_t* __restrict__ order, uint64_t t0,
                                           uint32_t recw, const RKT& rkT, uint32_t sbox,
-                                          const KM& km) {
+                                          const KM& km, uint32_t tid = threadIdx.x) {
     static_assert(LPR == 8 || LPR == 16 || LPR == 32 || LPR == 64, "lanes per record");
     static_assert(LPR == 8 || LPR == 32 || !TROLE, "the T-table role runs octets or pairs");
     constexpr uint32_t kM = LPR - 1, kS = LPR == 8 ? 3 : LPR == 16 ? 4 : LPR == 32 ? 5 : 6;
@@ -271,7 +272,7 @@ __device__ __forceinline__ void octet_job(const KC& kc, const tg_batch& b,
     constexpr uint32_t kShortMax = TG_KT_SHORT_MAX;
     RoleProbe pr;   // (measurement build TG_ROLE_PROBE; otherwise empty)
     if constexpr (LPR == 8) pr.start();
-    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t lane = tid & 63u;
     const uint32_t l = lane & kM;
     const uint64_t t = t0 + (lane >> kS);
     const bool valid = t < b.n;
@@ -582,9 +583,12 @@ __device__ __forceinline__ void octet_job(const KC& kc, const tg_batch& b,
     }
     diff = (uint32_t)__shfl((int)diff, (int)(lane & ~kM & 63u), 64);
     if (valid && diff) {   // a rejected record's plaintext is zeroed: each lane its own blocks
+        // (rho from a fresh lane index: held until here, it was the open
+        // kernel's last spill)
+        const uint32_t rz = ((fresh_lane() & kM) + nc + 1u) & kM;
         const uint4 z = make_uint4(0, 0, 0, 0);
-        for (uint32_t blk = rho; blk < nfull; blk += LPR) store16(out + 16u * blk, z, aligned);
-        if (tail && (nfull & kM) == rho) store_partial(out + 16u * nfull, z, tail);
+        for (uint32_t blk = rz; blk < nfull; blk += LPR) store16(out + 16u * blk, z, aligned);
+        if (tail && (nfull & kM) == rz) store_partial(out + 16u * nfull, z, tail);
     }
 #if defined(TG_ROLE_PROBE)
     if constexpr (LPR == 8) {
@@ -670,9 +674,21 @@ __global__ void tail_probe_print() {
 }
 #endif
 
+// The thread index passes through an empty asm at the top of every job, so
+// the per-lane values derived from it (lane fields, LDS row offsets of the
+// rotated GHASH tables, T-table copy offsets) are recomputed per job instead
+// of being hoisted out of the persistent loop and held across it -- where
+// they were spilled to scratch.
+// The index itself is rebuilt from the wave number (an SGPR) and the lane's
+// mbcnt inside an asm, so no VGPR holds it across the loop either.
+#if defined(TG_HY_HOIST)   // A/B builds: the compiler's hoisting (round 5)
+__device__ __forceinline__ uint32_t hy_tid(uint32_t) { return threadIdx.x; }
+#else
+__device__ __forceinline__ uint32_t hy_tid(uint32_t wave) { return (wave << 6) | fresh_lane(); }
+#endif
 template <int NR, bool OPEN, int THREADS>
 __global__ __launch_bounds__(THREADS) void gcm_hy_kernel(const GcmKeyDev* __restrict__ key,
-                                                            const tg_batch* bp,
+                                                            const tg_batch* __restrict__ bp,
                                                             const uint32_t* __restrict__ order,
                                                             uint32_t* __restrict__ queue,
                                                             uint32_t nt, uint32_t prio,
@@ -690,7 +706,6 @@ __global__ __launch_bounds__(THREADS) void gcm_hy_kernel(const GcmKeyDev* __rest
 #endif
     const uint64_t njobs = (bp->n + 7) / 8;
     const uint32_t recw = kHyRecBase + wave * kRecArea;
-    const uint4 jw = lds_u128(kHyJt + ((threadIdx.x & 15u) << 4));
 #if defined(TG_ROLE_PROBE)
     const uint64_t rp_t0 = __builtin_amdgcn_s_memtime();
     uint64_t rp_grab = 0;
@@ -712,8 +727,10 @@ __global__ __launch_bounds__(THREADS) void gcm_hy_kernel(const GcmKeyDev* __rest
             if (job >= njobs) break;
             asm volatile("" ::: "memory");
             const tg_batch b = *bp;
-            octet_job<NR, OPEN, true>(SingleKeyRowCtx{key, jw, masks}, b, order, 8ull * job, recw, rk,
-                                      kHySbox, bs8::KeyPlanesVmemFolded{{krows}});
+            const uint32_t tid = hy_tid(wave);
+            const uint4 jw = lds_u128(kHyJt + ((tid & 15u) << 4));
+            octet_job<NR, OPEN, true>(SingleKeyRowCtx{key, jw, masks, tid}, b, order, 8ull * job, recw, rk,
+                                      kHySbox, bs8::KeyPlanesVmemFolded{{krows}}, tid);
         }
     } else {
         // The key rows by scalar loads (SGPR operands: the T gates issue at
@@ -730,9 +747,11 @@ __global__ __launch_bounds__(THREADS) void gcm_hy_kernel(const GcmKeyDev* __rest
             if (job >= njobs) break;
             asm volatile("" ::: "memory");
             const tg_batch b = *bp;
+            const uint32_t tid = hy_tid(wave);
+            const uint4 jw = lds_u128(kHyJt + ((tid & 15u) << 4));
             octet_job<NR, OPEN, false, bs8::KeyPlanesVmemFolded, SingleKeyRowCtx, (THREADS < 1024)>(
-                SingleKeyRowCtx{key, jw, masks}, b, order, 8ull * job, recw, none, kHySbox,
-                bs8::KeyPlanesVmemFolded{{krows}});
+                SingleKeyRowCtx{key, jw, masks, tid}, b, order, 8ull * job, recw, none, kHySbox,
+                bs8::KeyPlanesVmemFolded{{krows}}, tid);
         }
     }
 #if defined(TG_TAIL_PROBE)

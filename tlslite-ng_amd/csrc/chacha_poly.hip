@@ -126,6 +126,7 @@ __device__ __forceinline__ uint32_t wave_max_octet(uint32_t v) {
 struct WaveTile {
     uint4 row[64][8];
     uint4 ptr[64];  // {in lo, in hi, out lo, out hi}
+    uint4 skey[64]; // each lane's Poly1305 s, parked across the tile loop (chacha_kernel)
 };
 constexpr int kWavesPerGroup = kChachaThreads / 64;
 
@@ -379,7 +380,7 @@ __global__ __launch_bounds__(kChachaThreads, MINW) void chacha_kernel(
     // Lanes past the end of the batch stay alive to serve the wave's
     // coalesced transfers, but work on a clamped record and never store.
     const uint64_t t = i_raw < b.n ? i_raw : b.n - 1;
-    const uint64_t i = order ? order[t] : t;   // planner.hip: records longest first
+    uint64_t i = order ? order[t] : t;   // planner.hip: records longest first
     uint32_t ki = 0;
     if (MULTIKEY) {
         ki = b.key_idx[i];
@@ -396,9 +397,9 @@ __global__ __launch_bounds__(kChachaThreads, MINW) void chacha_kernel(
 
     const uint8_t* in = rec_in(b, i);
     uint8_t* out = rec_out(b, i);
-    const uint32_t len = rec_len(b, i);
+    uint32_t len = rec_len(b, i);
     const uint8_t* ad = rec_aad(b, i);
-    const uint32_t alen = rec_aad_len(b, i);
+    uint32_t alen = rec_aad_len(b, i);
     const bool aligned = (((uintptr_t)in | (uintptr_t)out) & 15) == 0;
     const uint4 nv = load_partial(b.nonce + 12 * i, 12);
     // the tile stores a row only with a non-null output pointer
@@ -433,13 +434,34 @@ __global__ __launch_bounds__(kChachaThreads, MINW) void chacha_kernel(
         const uint8_t* tile_in = valid ? in : reinterpret_cast<const uint8_t*>(((uint64_t)in_hi << 32) | in_lo);
         t.ptr[lane] = make_uint4((uint32_t)(uintptr_t)tile_in, (uint32_t)((uintptr_t)tile_in >> 32),
                                  (uint32_t)(uintptr_t)tile_out, (uint32_t)((uintptr_t)tile_out >> 32));
+        t.skey[lane] = make_uint4(p.p0, p.p1, p.p2, p.p3);
         __builtin_amdgcn_wave_barrier();
         if (DMA)
             tiled_blocks_dma<OPEN>(t, lane, k, nv, jmin, p, ks);
         else
             tiled_blocks<OPEN>(t, lane, k, nv, jmin, p, ks);
         j0 = jmin;
+        const uint4 sk = t.skey[lane];
+        p.p0 = sk.x; p.p1 = sk.y; p.p2 = sk.z; p.p3 = sk.w;
     }
+#if !defined(TG_CHACHA_KEEP_FIELDS)
+    // The record's index and fields are read again here instead of being kept
+    // live across the tile loop, which does not use them: holding them cost
+    // 9 (seal) / 12 (open) VGPRs of spills to scratch, i.e. a private segment
+    // and runtime scratch memory for every queue the kernel runs on
+    // (profiles/r06/x10/stream_mem.jsonl).  The index goes through an empty asm
+    // so the compiler cannot reuse the loads above (and keep their results).
+    {
+        uint64_t tr = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+        tr = tr < b.n ? tr : b.n - 1;
+        __asm__ volatile("" : "+v"(tr));
+        i = order ? order[tr] : tr;
+        in = rec_in(b, i);
+        out = rec_out(b, i);
+        len = rec_len(b, i);
+        alen = rec_aad_len(b, i);
+    }
+#endif
     if (valid) {
         if (aligned) {
             full_blocks<OPEN, true>(k, nv, in, out, j0, nfull, p, ks);

@@ -53,6 +53,16 @@ struct MeasurementMark {
 }  // namespace
 #endif
 
+// The lane's index within its wave, computed inside an asm: the compiler can
+// neither hoist it out of a loop nor reuse an earlier copy, so the values
+// derived from it are recomputed where they are used instead of being held in
+// VGPRs across long loops (the persistent kernels spilled such values).
+__device__ __forceinline__ uint32_t fresh_lane() {
+    uint32_t l;
+    __asm__ volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(l));
+    return l;
+}
+
 // 16 tables x 256 entries x 16 bytes: M_j[b] = b * x^(8j) * H, so that
 // X * H = XOR_j M_j[byte_j(X)] (GCM bit order, aesgcm.py:8-14).
 constexpr int kGhashEntries = 16 * 256;

@@ -8,8 +8,10 @@ before and after, and the scratch the library itself holds
 
   torch      a torch elementwise kernel (no library call, no private segment)
   nonces     tg_make_nonces (a library kernel with no private segment)
-  chacha     ChaCha20-Poly1305 batch (lane kernel: private segment 40 B)
-  aesgcm     AES-128-GCM batch (hybrid kernel: private segment 92 B)
+  chacha     ChaCha20-Poly1305 batch (lane kernel: private segment 40 B in
+             round 5, none since round 6)
+  aesgcm     AES-128-GCM batch (hybrid kernel: private segment 92 B in
+             round 5, none since round 6)
 
 usage: python tools/stream_mem_probe.py  -> one JSON line per kind
 """
