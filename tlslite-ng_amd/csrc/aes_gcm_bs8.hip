@@ -988,6 +988,14 @@ __device__ __forceinline__ uint32_t kth_tab(uint32_t w) {
     return w < 8 ? w * 8192u : 2u * 65536u + (w - 8u) * 8192u;
 }
 
+// The thread index per pair from a fresh lane index, as in gcm_hy_kernel:
+// 154 -> 142 VGPRs, config 4 +0.4 / +0.6 % in two alternations
+// (profiles/r06/y3/c4_ab.txt).
+#if defined(TG_KTH_HOIST)   // A/B builds: the compiler's hoisting (round 5)
+#define KTH_TID(w) threadIdx.x
+#else
+#define KTH_TID(w) hy_tid(w)
+#endif
 template <int NR, bool OPEN>
 __global__ __launch_bounds__(kKthThreads) void gcm_kth_kernel(const GcmTableKey* __restrict__ keys,
                                                              const uint4* __restrict__ hpow,
@@ -1045,12 +1053,13 @@ __global__ __launch_bounds__(kKthThreads) void gcm_kth_kernel(const GcmTableKey*
             for (uint32_t pp = p0; pp < p1; pp += 2u) {   // the planned job's pairs
                 tg_batch bj = b;
                 bj.n = pp + 2u < p1 ? pp + 2u : p1;   // the pair's slots are pp .. bj.n - 1
+                const uint32_t tid = KTH_TID(wave);
                 if (wave < nt)
                     octet_job<NR, OPEN, true, bs8::KeyPlanesVmemFolded, TableKeyCtx, false, 32, RkTab>(
-                        kc, bj, order, pp, recw, RkTab{keys[k].rk, rot + 16u * k}, kKthSbox, km);
+                        kc, bj, order, pp, recw, RkTab{keys[k].rk, rot + 16u * k}, kKthSbox, km, tid);
                 else
                     octet_job<NR, OPEN, false, bs8::KeyPlanesVmemFolded, TableKeyCtx, false, 32, RkTab>(
-                        kc, bj, order, pp, recw, RkTab{keys[k].rk, rot + 16u * k}, kKthSbox, km);
+                        kc, bj, order, pp, recw, RkTab{keys[k].rk, rot + 16u * k}, kKthSbox, km, tid);
             }
         }
         if (tail) break;
