@@ -59,6 +59,9 @@ def main():
     ok = int(status.sum()) == n and bool(torch.equal(back, inp))
     res["roundtrip_ok"] = ok
     res["lib"] = os.environ.get("TLSGPU_LIB", "tree")
+    opts = {k: v for k, v in os.environ.items() if k.startswith("TLSGPU_") and k != "TLSGPU_LIB"}
+    if opts:
+        res["options"] = opts
     print(json.dumps(res), flush=True)
     sys.exit(0 if ok else 3)
 
