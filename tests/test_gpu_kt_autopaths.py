@@ -88,24 +88,15 @@ def test_one_length_key_table_whole_batch(torch, tg, oracle_mod, n, L, klen):
     _tamper_open(torch, tg, table, sealed, n, L, SL, nonces, aad, kidx, inp, bad)
 
 
-@pytest.mark.parametrize("opts", [{}, {"kt_lpr": 32}, {"gcm_table_variant": 14}])
-def test_planner_64bit_keys(torch, tg, oracle_mod, opts):
-    """nkeys = 2^17 + 1 makes the plan sort on 64-bit keys (key | length
-    packed beyond 32 bits).  Per-record lengths around the 2 048-byte split,
-    key indices over the whole table and some out of range (planned into
-    the lane kernel's tail and skipped: open status 0).  In-range records
-    against the oracle, then opened back."""
+def _planned_roundtrip(torch, tg, oracle_mod, opts, nkeys, lens, ki, out_of_range):
+    """Seal a mixed-length key-table batch on the planned path, in-range
+    records against the oracle, then open it back (out-of-range key indices:
+    skipped, status 0, plaintext zeroed)."""
     from batchpack import HostBatch
-    nkeys = (1 << 17) + 1
-    rng = np.random.default_rng(0x64b)
+    rng = np.random.default_rng(nkeys)
     keys = rng.integers(0, 256, (nkeys, 16), dtype=np.uint8)
-    lens = list(rng.integers(0, 5000, 5000)) + [2047, 2048, 2049, 16384, 16385, 0, 1]
     hb = HostBatch(lens, payload_seed=9, align=16, aad_mode="tls12", key_count=2)
     n = hb.n
-    ki = rng.integers(0, nkeys, n).astype(np.uint32)
-    ki[:3] = [0, nkeys - 1, nkeys - 2]
-    out_of_range = [5, 17, n - 2]
-    ki[out_of_range] = [nkeys, nkeys + 12345, 0xfffffff0]
     hb.key_idx = ki
     table = tg.KeyTable("aesgcm", [bytes(k) for k in keys])
     d = hb.to_device(torch)
@@ -136,3 +127,46 @@ def test_planner_64bit_keys(torch, tg, oracle_mod, opts):
             assert np.array_equal(back[o:o + L], hb.inp[o:o + L]), ("open", i)
         else:
             assert not back[o:o + L].any(), ("skipped record not zeroed", i)
+
+
+@pytest.mark.parametrize("opts", [{}, {"kt_lpr": 32}, {"gcm_table_variant": 14}])
+def test_planner_64bit_keys(torch, tg, oracle_mod, opts):
+    """nkeys = 2^17 + 1 makes the plan sort on 64-bit keys (key | length
+    packed beyond 32 bits; above the counting plan's key limit).  Per-record
+    lengths around the 2 048-byte split, key indices over the whole table and
+    some out of range (planned into the lane kernel's tail and skipped: open
+    status 0).  In-range records against the oracle, then opened back."""
+    nkeys = (1 << 17) + 1
+    rng = np.random.default_rng(0x64b)
+    lens = list(rng.integers(0, 5000, 5000)) + [2047, 2048, 2049, 16384, 16385, 0, 1]
+    n = len(lens)
+    ki = rng.integers(0, nkeys, n).astype(np.uint32)
+    ki[:3] = [0, nkeys - 1, nkeys - 2]
+    out_of_range = [5, 17, n - 2]
+    ki[out_of_range] = [nkeys, nkeys + 12345, 0xfffffff0]
+    _planned_roundtrip(torch, tg, oracle_mod, opts, nkeys, lens, ki, out_of_range)
+
+
+@pytest.mark.parametrize("opts", [{}, {"kt_lpr": 32}, {"kt_lpr": 8}, {"gcm_table_variant": 14},
+                                  {"kt_overlap": -1}])
+def test_counting_plan_skewed_keys(torch, tg, oracle_mod, opts):
+    """The counting plan (planner.hip key_job_plan_counting, up to 2^17 keys):
+    records 0-299 on one key (about 265 of them long: above kBucketSortMax,
+    left in scatter order), 64 and 65 records on two more keys, 40 records of
+    one length on a fourth, the rest spread over 997 keys; lengths 0 .. 18 000
+    around the split, and out-of-range key indices, one on a 40 000-byte
+    record (the tail's length buckets clamp at 32 767).  Every in-range record
+    against the oracle, then opened back."""
+    nkeys = 997
+    rng = np.random.default_rng(0xc0de)
+    lens = list(rng.integers(0, 18000, 2600)) + [2047, 2048, 2049, 16384, 16385, 0, 1, 32766, 32767, 40000]
+    lens += [4096] * 40
+    n = len(lens)
+    ki = rng.integers(0, nkeys, n).astype(np.uint32)
+    ki[:300] = 3
+    ki[300:364] = 5
+    ki[364:429] = 7
+    ki[n - 40:] = 11
+    out_of_range = [400, 1000, 2609, n - 41]   # 2609: the 40 000-byte record
+    ki[out_of_range] = [nkeys, nkeys + 5, nkeys + 1, 0xffffffff]
+    _planned_roundtrip(torch, tg, oracle_mod, opts, nkeys, lens, ki, out_of_range)
