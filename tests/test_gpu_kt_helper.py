@@ -1,13 +1,15 @@
 """GPU: key-table batches on independent streams stay independent (ADVICE
 r05).
 
-A key-table AES-GCM batch of mixed lengths runs its long records on the
-key-table hybrid kernel and its short ones (< 2 048 B) on the lane kernel,
-which goes to a helper stream forked from the caller's stream
-(aes_gcm_bs8.hip launch_kt, api.hip helper_fork / helper_join).  Round 5 had
-ONE helper per device: a second caller's short records queued behind the
-first caller's, so the second caller's stream waited for the first one's.
-Here:
+A key-table AES-GCM batch of mixed lengths runs its long records on a
+key-grouped kernel.  The key-table hybrid (the default) takes the short
+records (< 2 048 B) itself once its long jobs are taken; with the bitsliced
+key-grouped kernel (option kt_hybrid -1) and the other long kernels, the
+short ones go to the lane kernel on a helper stream forked from the caller's
+stream (aes_gcm_bs8.hip launch_kt, api.hip helper_fork / helper_join).
+Round 5 had ONE helper per device: a second caller's short records queued
+behind the first caller's, so the second caller's stream waited for the
+first one's.  Here:
 
 * a caller whose stream is held up (a spin kernel ahead of its batch) does
   not hold up another caller's batch on another stream;
@@ -109,6 +111,14 @@ class KtJob(object):
 
 
 def test_held_up_caller_does_not_hold_up_another(torch, tg, oracle_mod):
+    """On the default path (the key-table hybrid takes its short records
+    itself: no helper stream).  With helper streams the same holds for the
+    library's own ordering (each caller in flight gets its own helper), but
+    whether another caller's work can pass a blocked stream also depends on
+    how the HIP runtime maps streams to hardware queues (GPU_MAX_HW_QUEUES,
+    4 per process on the test box): two streams on one hardware queue run in
+    order.  So the timing assertion is made where no helper is involved."""
+    tg.scratch_trim(0)
     a = KtJob(torch, tg, 1)
     b = KtJob(torch, tg, 2)
     sa, sb = torch.cuda.Stream(), torch.cuda.Stream()
@@ -128,8 +138,7 @@ def test_held_up_caller_does_not_hold_up_another(torch, tg, oracle_mod):
     a_pending = not done_a.query()
     torch.cuda.synchronize()
     assert a_pending, "stream B waited for stream A's work"
-    streams, busy = tg.helper_info()
-    assert busy == 0 and streams >= 2, (streams, busy)
+    assert tg.helper_info()[1] == 0
     for j in (a, b):
         j.open(tg, None)
     torch.cuda.synchronize()
@@ -137,7 +146,13 @@ def test_held_up_caller_does_not_hold_up_another(torch, tg, oracle_mod):
     b.check(torch, oracle_mod)
 
 
-def test_two_threads_key_tables_concurrent(torch, tg, oracle_mod):
+@pytest.mark.parametrize("opts", [{}, {"kt_hybrid": -1}])
+def test_two_threads_key_tables_concurrent(torch, tg, oracle_mod, opts):
+    with tg.options(**opts):
+        _two_threads(torch, tg, oracle_mod)
+
+
+def _two_threads(torch, tg, oracle_mod):
     jobs = [KtJob(torch, tg, 10 + t) for t in range(2)]
     errors = []
     barrier = threading.Barrier(2)

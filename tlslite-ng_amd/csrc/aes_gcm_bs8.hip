@@ -33,6 +33,7 @@
 
 #include "aes_bs8.h"
 #include "aes_round.h"
+#include "gcm_lane.h"
 #include "ghash.h"
 #include "options.h"
 
@@ -1007,7 +1008,8 @@ __global__ __launch_bounds__(kKthThreads) void gcm_kth_kernel(const GcmTableKey*
                                                              const uint32_t* __restrict__ nlong_p,
                                                              const uint4* __restrict__ masks,
                                                              const uint32_t* __restrict__ jobkey,
-                                                             uint32_t* __restrict__ queue, uint32_t nt) {
+                                                             uint32_t* __restrict__ queue, uint32_t nt,
+                                                             uint64_t nkeys, uint32_t lanes) {
     stage_te(reinterpret_cast<uint32_t*>(g_lds_bs8) + kTeBase / 4);
     stage_sbox(kKthSbox);
     __syncthreads();
@@ -1021,8 +1023,8 @@ __global__ __launch_bounds__(kKthThreads) void gcm_kth_kernel(const GcmTableKey*
         j0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)j0);
         if (j0 >= njobs) break;
         const uint32_t j1 = j0 + kKthChunk < njobs ? j0 + kKthChunk : njobs;
-        // the chunk's job bounds and keys in one round of loads (jobkey:
-        // kth_jobkey_kernel), not a dependent jobpos -> order -> key_idx
+        // the chunk's job bounds and keys in one round of loads (jobkey: from
+        // the plan, tg_key_job_plan), not a dependent jobpos -> order -> key_idx
         // chain per job
         // (chunk of two: the values by selects, so the loop body -- both
         // roles' code -- exists once)
@@ -1064,6 +1066,38 @@ __global__ __launch_bounds__(kKthThreads) void gcm_kth_kernel(const GcmTableKey*
         }
         if (tail) break;
     }
+    // The short records -- plan slots [nlong, n) -- once the long jobs are all
+    // taken: one record per lane, 64 per grab, T-table CTR and the table-free
+    // GHASH of the lane kernel (gcm_lane.h gcm_record), the lane's 256-counter
+    // window slot in this wave's GHASH table area (free from here on).  The
+    // CUs then stay busy to the end instead of running a separate lane kernel
+    // after the long one (round 6; TG_KTH_LANE_KERNEL: the separate kernel).
+    if (lanes) {
+        const uint32_t lane = threadIdx.x & 63u;
+        const uint32_t lane4 = ((lane & 31u) << 2) | kTeBase, win = tab + 16u * lane;
+        for (;;) {
+            uint32_t c0 = 0;
+            if (lane == 0) c0 = atomicAdd(queue + 1, 64u);
+            c0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)c0);
+            if ((uint64_t)nlong + c0 >= b.n) break;
+            const uint64_t t = (uint64_t)nlong + c0 + lane;
+            if (t >= b.n) continue;
+            const uint32_t i = gld(order, t), k = gld(b.key_idx, i);
+            if (k >= nkeys) {   // skipped (open: status 0; tg_launch_zero_skipped clears it)
+                if (OPEN && b.status) gst(b.status, i, (uint8_t)0);
+                continue;
+            }
+            const GcmTableKey* kp = keys + k;
+            RkRegs<NR> rk;   // this record's key: per-lane values
+#pragma unroll
+            for (int q = 0; q <= NR; ++q) {
+                const uint4 v = gload16(reinterpret_cast<const uint8_t*>(kp->rk + 4 * q));
+                rk.w[4 * q] = v.x; rk.w[4 * q + 1] = v.y; rk.w[4 * q + 2] = v.z; rk.w[4 * q + 3] = v.w;
+            }
+            const GhashClmul gh{gload16(reinterpret_cast<const uint8_t*>(kp->hn))};
+            gcm_record<NR, OPEN, 1, RkRegs<NR>, GhashClmul, true>(b, i, lane4, rk, gh, win);
+        }
+    }
 }
 
 // E_K(J0) of every long record of a key-table plan, by plan slot (slots
@@ -1103,18 +1137,6 @@ __global__ __launch_bounds__(1024) void kt_mask_kernel(const GcmTableKey* __rest
             gstore16(reinterpret_cast<uint8_t*>(masks + 2 * t + 1),
                      aes_block<NR>(lane4, rk, make_uint4(nv.x, nv.y, nv.z, bswap32(nc + 1u))));
     }
-}
-
-// Per job of a key-table plan, the key of its records (the plan groups a
-// job's records by key): jobkey[j] = key_idx[order[jobpos[j]]] for the long
-// jobs (jobpos[j] < nlong); tail jobs are never read.
-__global__ void kth_jobkey_kernel(const uint32_t* __restrict__ jobpos, const uint32_t* __restrict__ njobs_p,
-                                  const uint32_t* __restrict__ nlong_p, const uint32_t* __restrict__ order,
-                                  const uint32_t* __restrict__ key_idx, uint32_t* __restrict__ jobkey) {
-    const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (j >= *njobs_p) return;
-    const uint32_t p0 = jobpos[j];
-    jobkey[j] = p0 < *nlong_p ? key_idx[order[p0]] : 0xffffffffu;
 }
 
 // Per key, the T-table waves' rotated round keys: rot[16 k + r] = rotr8 of
@@ -1160,12 +1182,12 @@ template <int NR, bool OPEN>
 int launch_kth(const GcmTableKey* keys, const uint4* hpow, const uint32_t* planes, const uint4* rot,
                const tg_batch& b, hipStream_t s, const uint32_t* order, const uint32_t* jobpos,
                const uint32_t* njobs, const uint32_t* nlong, uint32_t* queue, uint4* masks,
-               uint32_t* jobkey) {
+               uint32_t* jobkey, uint64_t nkeys, bool lanes) {
     const int t = opt(kOptKtT);
     if (t < 0 || t > kKthWaves) return TG_EINVAL;
     const uint32_t nt = t ? (uint32_t)t : (uint32_t)kKthTDefault;
     if (lds_attr((const void*)gcm_kth_kernel<NR, OPEN>, (int)kKthLds)) return TG_EHIP;
-    if (hipMemsetAsync(queue, 0, 4, s) != hipSuccess) return TG_EHIP;
+    if (hipMemsetAsync(queue, 0, 8, s) != hipSuccess) return TG_EHIP;   // long jobs, lane records
 #if defined(TG_KTH_NO_MASK)   // A/B builds: every wave computes its records' masks
     masks = nullptr;
 #else
@@ -1174,11 +1196,9 @@ int launch_kth(const GcmTableKey* keys, const uint4* hpow, const uint32_t* plane
     hipLaunchKernelGGL((kt_mask_kernel<NR>), dim3((unsigned)(wgs < cus ? wgs : cus)), dim3(1024), 65536, s, keys,
                        b, order, nlong, masks);
 #endif
-    // every job holds at least one plan slot, so njobs <= n
-    hipLaunchKernelGGL(kth_jobkey_kernel, dim3((unsigned)((b.n + 256) / 256)), dim3(256), 0, s, jobpos, njobs,
-                       nlong, order, b.key_idx, jobkey);
     hipLaunchKernelGGL((gcm_kth_kernel<NR, OPEN>), dim3((unsigned)device_cus()), dim3(kKthThreads), kKthLds, s,
-                       keys, hpow, planes, rot, b, order, jobpos, njobs, nlong, masks, jobkey, queue, nt);
+                       keys, hpow, planes, rot, b, order, jobpos, njobs, nlong, masks, jobkey, queue, nt, nkeys,
+                       lanes ? 1u : 0u);
     return hipGetLastError() == hipSuccess ? TG_OK : TG_EHIP;
 }
 
@@ -1228,7 +1248,7 @@ int launch_kt(const GcmTableKey* keys, uint64_t nkeys, const uint4* hpow, const 
     if (rc) return rc;
     const size_t so = (b.n * 4 + 255) & ~(size_t)255, sj = ((b.n + 1) * 4 + 255) & ~(size_t)255;
     // the key-table hybrid's per-slot tag masks (kt_mask_kernel) after the plan
-    const size_t sm = hybrid && lpr == 32 ? b.n * 32 + (b.n + 1) * 4 : 0;   // + kth_jobkey_kernel's keys
+    const size_t sm = hybrid && lpr == 32 ? b.n * 32 + (b.n + 1) * 4 : 0;   // + the jobs' keys
     const size_t po = (so + sj + 256 + plan + 255) & ~(size_t)255;
     uint8_t* buf = nullptr;
     if (stream_alloc((void**)&buf, po + sm, s)) return TG_EHIP;
@@ -1236,13 +1256,22 @@ int launch_kt(const GcmTableKey* keys, uint64_t nkeys, const uint4* hpow, const 
     uint32_t* jobpos = reinterpret_cast<uint32_t*>(buf + so);
     uint32_t* njobs = reinterpret_cast<uint32_t*>(buf + so + sj);
     uint32_t* nlong = njobs + 1;
+    uint32_t* jobkey = sm ? reinterpret_cast<uint32_t*>(buf + po + b.n * 32) : nullptr;
     rc = tg_key_job_plan(b.key_idx, b.len, b.fixed_len, b.n, nkeys, split, jobsz, order, jobpos, njobs, nlong,
-                         buf + so + sj + 256, &plan, s);
+                         buf + so + sj + 256, &plan, s, jobkey);
     // the lane kernel's records (plan slots [nlong, n)) are disjoint from the
     // long kernel's: it runs on a helper stream, forked after the plan and
     // joined before the scratch goes back (option kt_overlap -1: one stream)
+    // the key-table hybrid takes the short records itself once its long jobs
+    // are taken (gcm_kth_kernel); the other long kernels leave them to the
+    // lane kernel
+#if defined(TG_KTH_LANE_KERNEL)   // A/B builds: the separate lane kernel beside the hybrid
+    const bool kth_lanes = false;
+#else
+    const bool kth_lanes = hybrid && lpr == 32 && split != 0xffffffffu;
+#endif
     hipStream_t s2 = nullptr;
-    if (!rc && split != 0xffffffffu && opt(kOptKtOverlap) >= 0) rc = helper_fork(s, &s2);
+    if (!rc && split != 0xffffffffu && !kth_lanes && opt(kOptKtOverlap) >= 0) rc = helper_fork(s, &s2);
     if (!rc && split != 0xffffffffu) {
         switch (lpr) {
             case 0:   // the long records one per wavefront (plan slots [0, nlong))
@@ -1252,15 +1281,15 @@ int launch_kt(const GcmTableKey* keys, uint64_t nkeys, const uint4* hpow, const 
             case 16: rc = launch_kt_jobs<NR, OPEN, 16>(keys, nkeys, hpow, planes, b, s, order, jobpos, njobs, nlong); break;
             case 32:
                 rc = hybrid ? launch_kth<NR, OPEN>(keys, hpow, planes, rot, b, s, order, jobpos, njobs, nlong,
-                                                   njobs + 16, reinterpret_cast<uint4*>(buf + po),
-                                                   reinterpret_cast<uint32_t*>(buf + po + b.n * 32))
+                                                   njobs + 16, reinterpret_cast<uint4*>(buf + po), jobkey, nkeys,
+                                                   kth_lanes)
                             : launch_kt_jobs<NR, OPEN, 32>(keys, nkeys, hpow, planes, b, s, order, jobpos, njobs,
                                                            nlong);
                 break;
             default: rc = launch_kt_jobs<NR, OPEN, 64>(keys, nkeys, hpow, planes, b, s, order, jobpos, njobs, nlong); break;
         }
     }
-    if (!rc) rc = tg_launch_gcm_table_lane(keys, nkeys, NR, b, OPEN, s2 ? s2 : s, order, nlong);
+    if (!rc && !kth_lanes) rc = tg_launch_gcm_table_lane(keys, nkeys, NR, b, OPEN, s2 ? s2 : s, order, nlong);
     // rejoin (also after a failed launch: the scratch must outlive both streams' work)
     if (s2 && helper_join(s2, s) && !rc) rc = TG_EHIP;
     if (stream_free(buf, s)) return TG_EHIP;

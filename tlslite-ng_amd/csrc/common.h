@@ -390,10 +390,12 @@ int tg_launch_zero_skipped(const tg_batch& b, uint64_t nkeys, hipStream_t s);
 // Key-grouped jobs of a key-table batch (planner.hip): records of at least
 // ``split`` bytes with key_idx < nkeys in front, grouped by key and cut into
 // jobs of at most jobsz (a power of two) records of one key; the rest
-// behind them from slot *nlong on, longest first.
+// behind them from slot *nlong on, longest first.  jobkey (optional, n + 1
+// entries): each job's key, ~0 for the tail's jobs.
 int tg_key_job_plan(const uint32_t* key_idx, const uint32_t* len, uint32_t fixed_len, uint64_t n,
                     uint64_t nkeys, uint32_t split, uint32_t jobsz, uint32_t* order, uint32_t* jobpos,
-                    uint32_t* njobs, uint32_t* nlong, void* scratch, size_t* bytes, hipStream_t s);
+                    uint32_t* njobs, uint32_t* nlong, void* scratch, size_t* bytes, hipStream_t s,
+                    uint32_t* jobkey = nullptr);
 // Key-table AES-GCM (aes_gcm_bs8.hip launch_kt): records of at least
 // ``split`` bytes through the key-grouped octet kernel (planes = per-key
 // bitsliced key rows, MixColumns-folded, tg_launch_kt_planes; hpow = the keys'

@@ -125,6 +125,17 @@ __global__ void kjp_scatter(const uint32_t* __restrict__ js, const uint32_t* __r
     }
 }
 
+// Per job of the radix plan, the key of its records: jobkey[j] =
+// key_idx[order[jobpos[j]]] for the long jobs, ~0 for the tail's.
+__global__ void kjp_jobkey(const uint32_t* __restrict__ jobpos, const uint32_t* __restrict__ njobs_p,
+                           const uint32_t* __restrict__ nlong_p, const uint32_t* __restrict__ order,
+                           const uint32_t* __restrict__ key_idx, uint32_t* __restrict__ jobkey) {
+    const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= *njobs_p) return;
+    const uint32_t p0 = jobpos[j];
+    jobkey[j] = p0 < *nlong_p ? key_idx[order[p0]] : 0xffffffffu;
+}
+
 int bit_width(uint64_t v) {
     int b = 0;
     while (v) {
@@ -385,7 +396,8 @@ __device__ __forceinline__ void kbp_sort_small(uint32_t* __restrict__ order, con
 __global__ __launch_bounds__(256) void kbp_finish(const uint32_t* __restrict__ start, const uint32_t* __restrict__ jstart,
                            const uint32_t* __restrict__ len, uint64_t nkeys, uint32_t jobsz,
                            uint32_t* __restrict__ order, uint32_t* __restrict__ jobpos,
-                           const uint32_t* __restrict__ njobs, const uint32_t* __restrict__ nlong) {
+                           const uint32_t* __restrict__ njobs, const uint32_t* __restrict__ nlong,
+                           uint32_t* __restrict__ jobkey) {
     const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (t < nkeys) {
         const uint32_t s0 = start[t], m = start[t + 1] - s0;
@@ -411,16 +423,22 @@ __global__ __launch_bounds__(256) void kbp_finish(const uint32_t* __restrict__ s
             }
         }
         const uint32_t j0 = jstart[t];
-        for (uint32_t q = 0; q * jobsz < m; ++q) jobpos[j0 + q] = s0 + q * jobsz;
+        for (uint32_t q = 0; q * jobsz < m; ++q) {
+            jobpos[j0 + q] = s0 + q * jobsz;
+            if (jobkey) jobkey[j0 + q] = (uint32_t)t;
+        }
     }
     const uint32_t jl = jstart[nkeys], nl = *nlong, jt = *njobs - jl;
-    for (uint64_t q = t; q < jt; q += (uint64_t)gridDim.x * blockDim.x)
+    for (uint64_t q = t; q < jt; q += (uint64_t)gridDim.x * blockDim.x) {
         jobpos[jl + q] = nl + (uint32_t)q * jobsz;
+        if (jobkey) jobkey[jl + q] = 0xffffffffu;
+    }
 }
 
 int key_job_plan_counting(const uint32_t* key_idx, const uint32_t* len, uint32_t fixed_len, uint64_t n,
                           uint64_t nkeys, uint32_t split, uint32_t jobsz, uint32_t* order, uint32_t* jobpos,
-                          uint32_t* njobs, uint32_t* nlong, void* scratch, size_t* bytes, hipStream_t s) {
+                          uint32_t* njobs, uint32_t* nlong, void* scratch, size_t* bytes, hipStream_t s,
+                          uint32_t* jobkey) {
     // [key counters | tail counters | start | jstart], each 256-byte aligned
     // (the scan reads the counters 16 bytes at a time)
     const size_t bk = ru256(nkeys * 4), bc = bk + ru256(kTailBuckets * 4), bs = ru256((nkeys + 1) * 4);
@@ -448,7 +466,7 @@ int key_job_plan_counting(const uint32_t* key_idx, const uint32_t* len, uint32_t
                        cnt, tcnt, order);
     const uint64_t fthreads = nkeys > n / jobsz ? nkeys : n / jobsz + 1;
     hipLaunchKernelGGL(kbp_finish, dim3((unsigned)((fthreads + 255) / 256)), dim3(256), 0, s, start, jstart, len, nkeys,
-                       jobsz, order, jobpos, njobs, nlong);
+                       jobsz, order, jobpos, njobs, nlong, jobkey);
     return hipGetLastError() == hipSuccess ? TG_OK : TG_EHIP;
 }
 
@@ -463,21 +481,26 @@ int key_job_plan_counting(const uint32_t* key_idx, const uint32_t* len, uint32_t
 // from counting (key_job_plan_counting), otherwise from a radix sort.
 int tg_key_job_plan(const uint32_t* key_idx, const uint32_t* len, uint32_t fixed_len, uint64_t n,
                     uint64_t nkeys, uint32_t split, uint32_t jobsz, uint32_t* order, uint32_t* jobpos,
-                    uint32_t* njobs, uint32_t* nlong, void* scratch, size_t* bytes, hipStream_t s) {
+                    uint32_t* njobs, uint32_t* nlong, void* scratch, size_t* bytes, hipStream_t s,
+                    uint32_t* jobkey) {
     if (jobsz == 0 || (jobsz & (jobsz - 1u))) return TG_EINVAL;
 #if !defined(TG_PLAN_RADIX)   // A/B builds: the radix-sorted plan at any key count
     if (nkeys <= kBucketMaxKeys && n < 0xffffffffull)
         return key_job_plan_counting(key_idx, len, fixed_len, n, nkeys, split, jobsz, order, jobpos, njobs, nlong,
-                                     scratch, bytes, s);
+                                     scratch, bytes, s, jobkey);
 #endif
     // 32-bit keys when the key index (tail marker nkeys included) leaves at
     // least 15 bits for the length: 2^14 + 256, the longest TLS record, fits
     const int kb = bit_width(nkeys);
-    if (kb <= 17)
-        return key_job_plan<uint32_t>(key_idx, len, fixed_len, n, nkeys, split, jobsz, order, jobpos, njobs,
-                                      nlong, scratch, bytes, s, 32 - kb);
-    return key_job_plan<uint64_t>(key_idx, len, fixed_len, n, nkeys, split, jobsz, order, jobpos, njobs, nlong,
-                                  scratch, bytes, s, 32);
+    const int rc = kb <= 17 ? key_job_plan<uint32_t>(key_idx, len, fixed_len, n, nkeys, split, jobsz, order, jobpos,
+                                                     njobs, nlong, scratch, bytes, s, 32 - kb)
+                            : key_job_plan<uint64_t>(key_idx, len, fixed_len, n, nkeys, split, jobsz, order, jobpos,
+                                                     njobs, nlong, scratch, bytes, s, 32);
+    if (rc || !scratch || !jobkey) return rc;
+    // every job holds at least one plan slot, so njobs <= n
+    hipLaunchKernelGGL(kjp_jobkey, dim3((unsigned)((n + 256) / 256)), dim3(256), 0, s, jobpos, njobs, nlong, order,
+                       key_idx, jobkey);
+    return hipGetLastError() == hipSuccess ? TG_OK : TG_EHIP;
 }
 
 namespace {
