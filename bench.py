@@ -566,11 +566,14 @@ def c4_traffic(path, op):
         return None
     with open(path) as f:
         ks = json.load(f).get("kernels", {})
-    parts = [ks.get("c4_kt_" + op), ks.get("c4_lane_" + op)]
-    if not all(parts):
+    kt, lane = ks.get("c4_kt_" + op), ks.get("c4_lane_" + op)
+    if not kt:
         return None
-    kernels = {"long_records (gcm_kth_kernel)": round(parts[0]["hbm_bytes"]),
-               "gcm_table_vkernel": round(parts[1]["hbm_bytes"])}
+    if lane:   # a separate lane kernel for the short records (before round 6's fusion)
+        kernels = {"long_records (gcm_kth_kernel)": round(kt["hbm_bytes"]),
+                   "gcm_table_vkernel": round(lane["hbm_bytes"])}
+    else:      # the key-table hybrid takes the short records too
+        kernels = {"all_records (gcm_kth_kernel)": round(kt["hbm_bytes"])}
     # the per-record keystream precompute and per-job keys (round 4), one
     # launch each per seal or open, when the summary has them
     for lab, name in (("c4_masks", "kt_mask_kernel"), ("c4_jobkey", "kth_jobkey_kernel")):
