@@ -1228,12 +1228,13 @@ int launch_kt_jobs(const GcmTableKey* keys, uint64_t nkeys, const uint4* hpow, c
 // (aes_gcm.hip gcm_table_vkernel) over the tail of the same plan, which the
 // planner leaves sorted by length, longest first.  split 0: every in-range
 // record takes the long kernel; split ~0u: every record the lane kernel.
-// The lane kernel runs on a helper stream of the caller's stream (api.hip
-// helper_fork / helper_join: idle or last used by this caller, so two
-// callers never chain through one helper), forked after the plan and joined
-// before the scratch goes back: the CUs the long kernel's tail leaves idle
-// take lane-kernel workgroups instead of waiting for the whole grid
-// (+0.4 %, profiles/r05/r5z/).  Option kt_overlap -1: one stream.
+// The key-table hybrid (lpr 32, the default) runs the lane kernel's routine
+// itself over those records once its long jobs are taken: a separate lane
+// kernel ran 250-610 us alone after it (round 6, profiles/r06/z3/).  Beside
+// the other long kernels the lane kernel runs on a helper stream of the
+// caller's stream (api.hip helper_fork / helper_join: idle or last used by
+// this caller, so two callers never chain through one helper).  Option
+// kt_overlap -1: one stream.
 template <int NR, bool OPEN>
 int launch_kt(const GcmTableKey* keys, uint64_t nkeys, const uint4* hpow, const uint32_t* planes,
               const uint4* rot, const tg_batch& b, hipStream_t s, uint32_t split, int lpr, bool hybrid) {
@@ -1259,12 +1260,11 @@ int launch_kt(const GcmTableKey* keys, uint64_t nkeys, const uint4* hpow, const 
     uint32_t* jobkey = sm ? reinterpret_cast<uint32_t*>(buf + po + b.n * 32) : nullptr;
     rc = tg_key_job_plan(b.key_idx, b.len, b.fixed_len, b.n, nkeys, split, jobsz, order, jobpos, njobs, nlong,
                          buf + so + sj + 256, &plan, s, jobkey);
-    // the lane kernel's records (plan slots [nlong, n)) are disjoint from the
-    // long kernel's: it runs on a helper stream, forked after the plan and
-    // joined before the scratch goes back (option kt_overlap -1: one stream)
-    // the key-table hybrid takes the short records itself once its long jobs
-    // are taken (gcm_kth_kernel); the other long kernels leave them to the
-    // lane kernel
+    // The short records (plan slots [nlong, n)): the key-table hybrid takes
+    // them itself once its long jobs are taken (gcm_kth_kernel).  With the
+    // other long kernels they go to the lane kernel, on a helper stream forked
+    // after the plan and joined before the scratch goes back (its records are
+    // disjoint from the long kernel's; option kt_overlap -1: one stream).
 #if defined(TG_KTH_LANE_KERNEL)   // A/B builds: the separate lane kernel beside the hybrid
     const bool kth_lanes = false;
 #else
