@@ -202,6 +202,11 @@ constexpr uint64_t kPlanMinRecords = 2049;
 // Key-table AES-GCM: records of at least this many bytes take the
 // key-grouped octet kernel, shorter ones the lane kernel (option kt_split).
 constexpr uint32_t kKtSplitDefault = 2048;
+// With the short records inside the key-table hybrid (its lane loop runs
+// beside the long jobs instead of after them) the split moves down: config 4
+// 674-676 GiB/s at 1 024 against 663-668 at 2 048, 672-673 at 768 / 1 536,
+// 663-664 at 512 (profiles/r06/s2/).
+constexpr uint32_t kKtSplitFused = 1024;
 // Small key-table batches -- at most this many records, or one length with
 // at most this many bytes in all -- run one record per wavefront (the wave
 // kernel, table-free GHASH, no plan): 0.014 / 0.023 / 0.099 ms for 1 / 2 048 /
@@ -235,7 +240,8 @@ int launch_gcm_table(tg_key* k, const tg_batch& b, bool open, hipStream_t s) {
     switch (tg::opt(tg::kOptGcmTableVariant)) {
         case 0: {
             const int sp = tg::opt(tg::kOptKtSplit);
-            split = sp > 0 ? (uint32_t)sp : kKtSplitDefault;
+            split = sp > 0 ? (uint32_t)sp
+                  : lpr == 32 && tg::opt(tg::kOptKtHybrid) >= 0 ? kKtSplitFused : kKtSplitDefault;
             // small batches (unless the split or the long-record kernel is forced)
             if (sp == 0 && o == 0 &&
                 (b.n <= kKtWaveMaxRecords || (!b.len && b.n * (uint64_t)b.fixed_len <= kKtWaveMaxBytes)))
