@@ -974,10 +974,14 @@ constexpr size_t kKthLds = kKthRec + kKthWaves * kKthRecArea;
 // is 2 kKthGroup records): its waves run them pair by pair with one table
 // build.  kKthChunk planned jobs per grab.
 #if !defined(TG_KTH_GROUP)
-// 2: two pairs of one key per grab, one table build; against two planned
-// pairs per grab (1): 666.6-668.0 vs 663.6-665.0 GiB/s, 4: 657.7-659.9
-// (three rounds, profiles/r05/r5x/)
-#define TG_KTH_GROUP 2
+// Round 5 (separate lane kernel, 2 048-byte split): 2 pairs of one key per
+// grab 666.6-668.0 GiB/s, 1 pair (two planned per grab) 663.6-665.0, 4 pairs
+// 657.7-659.9 (profiles/r05/r5x/).  Round 6, with the short records inside
+// this kernel and the 1 024-byte split: 4 pairs 677.6-678.8 / 691.5-693.6
+// against 675.3-675.5 / 689.6-689.8 for 2 on two boxes, 8 pairs 671.0
+// (profiles/r06/g2/, g3/); 3 is refused by the plan (job sizes are powers
+// of two).
+#define TG_KTH_GROUP 4
 #endif
 constexpr uint32_t kKthGroup = TG_KTH_GROUP;
 // jobs per grab (1 / 2 / 4 / 8: 607 / 614 / 610 / 590 GiB/s, profiles/r04/r4j)
