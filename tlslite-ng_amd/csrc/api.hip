@@ -203,10 +203,12 @@ constexpr uint64_t kPlanMinRecords = 2049;
 // key-grouped octet kernel, shorter ones the lane kernel (option kt_split).
 constexpr uint32_t kKtSplitDefault = 2048;
 // With the short records inside the key-table hybrid (its lane loop runs
-// beside the long jobs instead of after them) the split moves down: config 4
-// 674-676 GiB/s at 1 024 against 663-668 at 2 048, 672-673 at 768 / 1 536,
-// 663-664 at 512 (profiles/r06/s2/).
-constexpr uint32_t kKtSplitFused = 1024;
+// beside the long jobs instead of after them) the split moves down.  With two
+// pairs per planned job: config 4 674-676 GiB/s at 1 024 against 663-668 at
+// 2 048 (profiles/r06/s2/); with four (TG_KTH_GROUP): 694.5-696.7 at 1 536,
+// 694.3-694.6 at 1 280, 693.1-693.8 at 1 792, 690.4 at 2 048, 688.4-689.1 at
+// 1 024, 681 at 768 (profiles/r06/s4/, s5/).
+constexpr uint32_t kKtSplitFused = 1536;
 // Small key-table batches -- at most this many records, or one length with
 // at most this many bytes in all -- run one record per wavefront (the wave
 // kernel, table-free GHASH, no plan): 0.014 / 0.023 / 0.099 ms for 1 / 2 048 /
